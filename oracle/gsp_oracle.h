@@ -1,0 +1,79 @@
+/*
+ * oracle/gsp_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of the reference's hot path, used only by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the CHECKER.  The product
+ * (gossip_protocol_amd/, libgossip_amd.so) never links, loads or calls anything here.
+ *
+ * Two restatements:
+ *   gsp_oracle_mp1_run    -- the reference MP1 simulator, byte-exact (dbg.log,
+ *                            msgcount.log, end-of-tick state).  Spec: SURVEY.md 3.2;
+ *                            pinned against oracle/_ref (the reference compiled from
+ *                            /root/reference) and the reference's committed dbg.log.
+ *   gsp_scale_oracle_*    -- the build-defined scale protocol (DESIGN.md "Scale mode"),
+ *                            full view, int32 hb/ts with absolute timestamps.  The reference
+ *                            cannot run at these sizes (EmulNet.h:10 MAX_NODES, MP1Node.cpp:245
+ *                            id<10 filter); the restatement follows the same per-entry rules.
+ */
+#ifndef GSP_ORACLE_H
+#define GSP_ORACLE_H
+#include <stdint.h>
+
+/* ---- glibc TYPE_3 rand() stream (glibc_rand.c) ---- */
+typedef struct {
+    uint32_t ring[34];
+    uint64_t pos;
+} gsp_glibc_rng;
+void gsp_glibc_srand(gsp_glibc_rng *g, uint32_t seed);
+int gsp_glibc_rand(gsp_glibc_rng *g);
+void gsp_glibc_stream(uint32_t seed, int32_t *out, int64_t n);
+
+/* ---- exact MP1 restatement (mp1_oracle.c) ---- */
+enum { GSP_RNG_GLIBC = 0, GSP_RNG_PHILOX = 1 };
+/* Returns 0 on success, <0 on error.  Any output path may be NULL. */
+int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int ticks,
+                       const char *dbg_path, const char *msgcount_path, const char *state_path,
+                       const char *stdout_path);
+
+/* ---- scale protocol restatement (scale_oracle.c) ---- */
+typedef struct {
+    int32_t n;          /* nodes (full view: V = n)                         */
+    int32_t fanout;     /* peers per sender per tick                        */
+    int32_t drop_pct;   /* drop iff philox_u31 % 100 < drop_pct             */
+    int32_t tremove;    /* removal timeout (reference TREMOVE = 20)         */
+    int32_t h0;         /* initial heartbeat of every pre-joined entry      */
+    int32_t fail_mode;  /* 0 none, 1 per-node Bernoulli, 2 contiguous block */
+    int32_t fail_tick;  /* nodes fail at the end of this tick               */
+    int32_t fail_ppm;   /* failure fraction, parts per million              */
+    uint64_t seed;
+} gsp_scale_cfg;
+
+typedef struct {
+    int64_t tick;
+    int64_t node_rounds; /* nodes that ran merge+ops this tick             */
+    int64_t merges;      /* sum over delivered GOSSIPs of 1 + |payload|    */
+    int64_t sent;        /* GOSSIP sends attempted (after peer choice)      */
+    int64_t dropped;     /* sends rejected by the drop draw                 */
+    int64_t delivered;   /* messages merged by an alive receiver            */
+    int64_t joins;       /* join events                                     */
+    int64_t removes;     /* remove events                                   */
+    uint64_t event_hash; /* sum of mix64(event key), order independent      */
+} gsp_tick_digest;
+
+typedef struct gsp_scale_oracle gsp_scale_oracle;
+gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg);
+void gsp_scale_oracle_destroy(gsp_scale_oracle *o);
+/* Advance one tick (t = 1, 2, ...).  Fills *d.  Returns 0 on success. */
+int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d);
+/* Row r as of the last completed tick: present/hb/ts for every column (absent: 0/0/0). */
+int gsp_scale_oracle_row(const gsp_scale_oracle *o, int32_t r, uint8_t *present, int32_t *hb,
+                         int32_t *ts);
+int gsp_scale_oracle_own_hb(const gsp_scale_oracle *o, int32_t r);
+int32_t gsp_scale_oracle_fail_tick(const gsp_scale_oracle *o, int32_t r);
+/* The messages (src, dst) sent at the last completed tick that survived the drop draw. */
+int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32_t *dst,
+                                  int64_t cap);
+
+uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x);
+
+#endif
