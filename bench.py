@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Headline benchmark: gossip node-rounds/s on the SCALE engine (BASELINE.json configs 3-4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One "step" = one protocol tick over the whole node population: every alive node merges
+the rows gossiped to it, bumps its heartbeat, runs the TREMOVE scan and gossips to `fanout`
+peers (the reference's nodeLoop, /root/reference/MP1Node.cpp:176-362, at scale).
+
+N = 1: BASELINE config 3 -- 65,536 nodes, full view (65,536 x 65,536 packed u16 table),
+       fanout 3, 1% random crash at t = 10, no drops; ticks 1..W warm up, W+1..W+K timed.
+N > 1: rows sharded over N GPUs (one process per GPU, torch.distributed over RCCL for the
+       barrier / timing reduction), see DESIGN.md "Multi-GPU".
+Prints ONE JSON line (rank 0) with the roofline of the fused tick kernel and the CPU
+baseline (the oracle restatement, timed on a bounded sample of the same workload).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+N_NODES = 65536
+FANOUT = 3
+FAIL_PPM = 10000            # 1 %
+FAIL_TICK = 10
+SEED = 0x5EED
+
+
+def cpu_baseline(budget_s=12.0):
+    """Oracle restatement (oracle/scale_oracle.c, 1 thread) on a bounded sample.
+
+    The full 65,536-wide table does not fit a CPU run of seconds, so the sample is the same
+    protocol at n = 4096 (full view, fanout 3, 1% crash at t = 10); its throughput in table
+    entries processed per second is converted to node-rounds/s of the 65,536-wide workload
+    (a node-round there processes 65,536 x (1 + k) entries, k = messages merged).
+    """
+    from tests.oracle_binding import ScaleOracle
+    n = 4096
+    orc = ScaleOracle(n, fanout=FANOUT, drop_pct=0, fail_mode=1, fail_tick=FAIL_TICK,
+                      fail_ppm=FAIL_PPM, seed=SEED)
+    t0 = time.perf_counter()
+    ticks = rounds = delivered = 0
+    while time.perf_counter() - t0 < budget_s and ticks < 60:
+        d = orc.step()
+        ticks += 1
+        rounds += d["node_rounds"]
+        delivered += d["delivered"]
+    el = time.perf_counter() - t0
+    orc.close()
+    entries = (rounds + delivered) * n          # own row + one sender row per message
+    entries_per_s = entries / el
+    k = delivered / max(rounds, 1)
+    per_round_65k = N_NODES * (1.0 + k)
+    return {"value": entries_per_s / per_round_65k, "unit": "node-rounds/s", "cores": 1,
+            "kind": "port",
+            "sample": "oracle/scale_oracle.c, n=4096 full view, %d ticks in %.1f s (%.3g entries/s), "
+                      "scaled to 65,536-wide rows" % (ticks, el, entries_per_s)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nodes", type=int, default=N_NODES)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
+
+    if world > 1:
+        from gossip_protocol_amd.shard import ShardedScaleEngine
+        eng = ShardedScaleEngine(args.nodes, fanout=FANOUT, fail_mode=FAIL_RANDOM,
+                                 fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM, seed=SEED,
+                                 max_ticks=args.warmup + args.steps, device=local)
+    else:
+        eng = ScaleEngine(args.nodes, fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK,
+                          fail_ppm=FAIL_PPM, seed=SEED, max_ticks=args.warmup + args.steps,
+                          device=local)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    eng.step(args.warmup)
+    eng.sync()
+    perf0 = eng.perf()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.step(args.steps)
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    eng.sync()
+    perf1 = eng.perf()
+
+    rounds = merges = delivered = 0
+    for t in range(args.warmup + 1, args.warmup + args.steps + 1):
+        d = eng.digest(t)
+        rounds += d["node_rounds"]
+        merges += d["merges"]
+        delivered += d["delivered"]
+    stride = -(-args.nodes // 2048) * 2048
+    launches = perf1["merge_launches"] - perf0["merge_launches"]
+    kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / max(launches, 1)
+    csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / max(launches, 1)
+    # algorithmic bytes per launch: own row read + write, one sender row per message
+    # (2-byte entries), one 4-byte CSR entry per message
+    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) / args.steps
+
+    if dist is not None:
+        t = torch.tensor([el, rounds, merges, bytes_per_launch, kern_ms], dtype=torch.float64,
+                         device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        el = tmax[0].item()
+        rounds, merges = tsum[1].item(), tsum[2].item()
+        kern_ms = tmax[4].item()
+
+    if rank == 0:
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(prof):
+            try:
+                traffic = json.load(open(prof)).get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "gossip node-rounds/sec (+ merge-kernel HBM GB/s, % peak)",
+            "value": rounds / el,
+            "unit": "node-rounds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak" if world > 1 else "weak",
+            "vs_baseline": None,
+            "dtype": "u16",
+            "data": "synthetic (pre-joined full-view membership, Philox peers/failures)",
+            "config": {"workload": "config3: %d nodes full view, fanout %d, 1%% random crash at "
+                                   "t=%d, no drops" % (args.nodes, FANOUT, FAIL_TICK),
+                       "nodes": args.nodes, "view": args.nodes, "fanout": FANOUT,
+                       "entry_bytes": 2, "parallelism": "rows%d" % world},
+            "merges_per_s": merges / el,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "scale_tick_kernel", "kernel_ms": kern_ms,
+                         "csr_ms": csr_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

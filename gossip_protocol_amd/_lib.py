@@ -1,0 +1,130 @@
+"""ctypes binding of libgossip_amd.so -- the C ABI declared in include/gossip/gossip.h.
+
+This is the same stub a maintainer would add on the reference side to call the engine
+from Python.  There is no fallback: if the in-tree shared library is
+missing, every entry point raises, so a GPU test can never pass on a CPU path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgossip_amd.so")
+
+c_int32 = ctypes.c_int32
+c_int64 = ctypes.c_int64
+c_uint64 = ctypes.c_uint64
+P = ctypes.POINTER
+
+
+class GspParams(ctypes.Structure):
+    _fields_ = [("max_nnb", c_int32), ("single_failure", c_int32), ("drop_msg", c_int32),
+                ("msg_drop_prob", ctypes.c_double), ("step_rate", ctypes.c_double),
+                ("max_msg_size", c_int32), ("en_buff_size", c_int32),
+                ("total_running_time", c_int32), ("tremove", c_int32),
+                ("id_filter_limit", c_int32)]
+
+
+class GspMemberView(ctypes.Structure):
+    _fields_ = [("id", c_int32), ("port", ctypes.c_int16), ("inited", ctypes.c_int8),
+                ("in_group", ctypes.c_int8), ("failed", ctypes.c_int8),
+                ("heartbeat", c_int64), ("n_members", c_int32)]
+
+
+class GspEntry(ctypes.Structure):
+    _fields_ = [("id", c_int32), ("port", ctypes.c_int16), ("heartbeat", c_int64),
+                ("timestamp", c_int64)]
+
+
+class GspExactStats(ctypes.Structure):
+    _fields_ = [("batches", c_int64), ("node_rounds", c_int64), ("merges", c_int64),
+                ("draws", c_int64), ("sends_admitted", c_int64), ("device_ms", ctypes.c_double)]
+
+
+class GspScaleParams(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("fanout", c_int32), ("drop_pct", c_int32),
+                ("tremove", c_int32), ("h0", c_int32), ("fail_mode", c_int32),
+                ("fail_tick", c_int32), ("fail_ppm", c_int32), ("seed", c_uint64),
+                ("max_ticks", c_int32)]
+
+
+class GspScaleDigest(ctypes.Structure):
+    _fields_ = [("tick", c_int64), ("node_rounds", c_int64), ("merges", c_int64),
+                ("sent", c_int64), ("dropped", c_int64), ("delivered", c_int64),
+                ("joins", c_int64), ("removes", c_int64), ("event_hash", c_uint64)]
+
+
+class GspScalePerf(ctypes.Structure):
+    _fields_ = [("ticks", c_int64), ("merge_launches", c_int64), ("merge_ms", ctypes.c_double),
+                ("csr_ms", ctypes.c_double), ("bytes_per_tick", ctypes.c_double)]
+
+
+# name -> (restype, argtypes); every name here must be exported (tests check it)
+SIGNATURES = {
+    "gsp_last_error": (ctypes.c_char_p, []),
+    "gsp_abi_version": (ctypes.c_int, []),
+    "gsp_device_count": (ctypes.c_int, []),
+    "gsp_replay_draw": (ctypes.c_uint32, [ctypes.c_uint32, c_uint64] + [ctypes.c_uint32] * 4),
+    "gsp_philox4x32_10": (ctypes.c_int, [P(ctypes.c_uint32), P(ctypes.c_uint32),
+                                         P(ctypes.c_uint32)]),
+    "gsp_params_default": (ctypes.c_int, [P(GspParams)]),
+    "gsp_params_from_conf": (ctypes.c_int, [ctypes.c_char_p, P(GspParams)]),
+    "gsp_create": (ctypes.c_int, [P(GspParams), ctypes.c_int, ctypes.c_int, c_uint64,
+                                  ctypes.c_char_p, P(ctypes.c_void_p)]),
+    "gsp_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_tick_recv": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32), c_int32]),
+    "gsp_tick_process": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32), P(ctypes.c_int8),
+                                        c_int32, c_int32]),
+    "gsp_rand": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
+    "gsp_log": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, ctypes.c_char_p]),
+    "gsp_set_failed": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32]),
+    "gsp_get_member": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspMemberView)]),
+    "gsp_member_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspEntry), c_int32,
+                                       P(c_int32)]),
+    "gsp_write_msgcount": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, c_int32]),
+    "gsp_counters": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), c_int32]),
+    "gsp_flush_log": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_log_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
+                                     P(ctypes.c_size_t)]),
+    "gsp_exact_stats_get": (ctypes.c_int, [ctypes.c_void_p, P(GspExactStats)]),
+    "gsp_scale_create": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, P(ctypes.c_void_p)]),
+    "gsp_scale_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_scale_step": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_scale_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_scale_tick": (ctypes.c_int, [ctypes.c_void_p, P(c_int32)]),
+    "gsp_scale_digest_get": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspScaleDigest)]),
+    "gsp_scale_row": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(ctypes.c_uint16), c_int32]),
+    "gsp_scale_own_hb": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
+    "gsp_scale_messages": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int64, P(c_int64)]),
+    "gsp_scale_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
+    "gsp_scale_set_timing": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
+}
+
+
+class GspError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree libgossip_amd.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GspError("%s is missing: run `make lib` (or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().gsp_last_error()
+        raise GspError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+    return rc

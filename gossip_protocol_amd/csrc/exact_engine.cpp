@@ -1,0 +1,560 @@
+// gossip_protocol_amd/csrc/exact_engine.cpp -- host side of the EXACT engine (C ABI).
+//
+// What stays on the host is the index-only bookkeeping whose result is defined by a
+// sequential order in the reference:
+//   * the EmulNet buffer and its delivery permutation (top-down scan with swap-with-last
+//     removal, EmulNet.cpp:144-177) -- per message only (src, dst, type, send batch);
+//   * the per-node FIFO queues (Queue.h:22-26), uploaded as CSR for each batch;
+//   * the dbg.log byte stream (Log.cpp:44-130), ordered from device event records.
+// Everything per member-list entry -- the recvCallBack merge, nodeLoopOps, list order,
+// the send lists, the draws, drop window and buffer admission -- runs in the HIP kernels
+// of exact_kernels.hip.
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "exact_kernels.hpp"
+#include "glibc_stream.hpp"
+#include "philox.hpp"
+
+namespace {
+
+constexpr int32_t kMaxNodes = 1024;    // one workgroup lane per column
+constexpr int32_t kMaxTicks = 3600;    // EmulNet.h:11 MAX_TIME
+constexpr int32_t kMsgHdrBytes = 40;   // sizeof(MessageHdr), MP1Node.h:43-47
+constexpr int32_t kEnMsgBytes = 16;    // sizeof(en_msg), EmulNet.h:23-30
+
+struct NetMsg {
+    int32_t src, dst, type;
+    int64_t send_batch;
+};
+
+// strcmp() over the two 6-byte addresses (EmulNet.cpp:154): the id bytes compared as a C
+// string, so e.g. ids 256 and 512 (both starting with a 0 byte) compare equal.
+bool addr_strcmp_equal(int32_t a, int32_t b) {
+    unsigned char x[5] = {0}, y[5] = {0};
+    std::memcpy(x, &a, 4);
+    std::memcpy(y, &b, 4);
+    for (int i = 0; i < 4; ++i) {
+        if (x[i] != y[i]) return false;
+        if (x[i] == 0) return true;
+    }
+    return true;  // continues into the port bytes, which are 0 for every node here
+}
+
+}  // namespace
+
+struct gsp_engine {
+    gsp_params p{};
+    int32_t n = 0;
+    int device = 0;
+    hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int rng_mode = 0;
+    uint64_t seed = 0;
+    gsp::GlibcStream glibc;
+    int64_t draws = 0;
+    int64_t batch_seq = 1;
+
+    std::vector<NetMsg> buf;                  // EmulNet::emulnet.buff
+    std::vector<std::vector<NetMsg>> queue;   // Member::mp1q per node
+    std::vector<int8_t> failed;
+    std::vector<int64_t> last_commit;
+    std::vector<int32_t> inited, in_group, own_hb, nlist;
+    std::vector<int32_t> recv_ctr;            // [(n+1) * kMaxTicks]
+
+    // dbg.log
+    std::string log;
+    FILE *logf = nullptr;
+    size_t log_flushed = 0;
+    bool log_first = true;
+
+    gsp_exact_stats stats{};
+
+    // device
+    gsp::DevBuf<int64_t> t_key, o_key, d_ev_raw;
+    gsp::DevBuf<int32_t> t_hb, t_ts, t_rank, t_state;
+    gsp::DevBuf<int32_t> o_hb, o_ts, o_rank, o_state;
+    gsp::DevBuf<int32_t> b_node, b_op, q_off, q_src, q_type, send_off, send_dst, send_type, send_cnt;
+    gsp::DevBuf<gsp::ExactEvent> events;
+    gsp::DevBuf<int32_t> counters;            // ev_count, adm_count, draws
+    gsp::DevBuf<unsigned long long> merges;
+    gsp::DevBuf<int32_t> stream, adm_src, adm_dst, adm_type, sent_ctr;
+
+    gsp::ExactTable table() {
+        gsp::ExactTable t;
+        t.key = t_key.p; t.hb = t_hb.p; t.ts = t_ts.p; t.rank = t_rank.p;
+        t.inited = t_state.p; t.in_group = t_state.p + n; t.own_hb = t_state.p + 2 * n;
+        t.nlist = t_state.p + 3 * n;
+        return t;
+    }
+
+    void append_line(int32_t node, int32_t tick, const char *text) {
+        if (log.empty()) {
+            // magic number: "%x\n" of the ASCII sum of "CS425" (Log.cpp:79-88)
+            int sum = 0;
+            for (const char *c = "CS425"; *c; ++c) sum += *c;
+            char m[16];
+            std::snprintf(m, sizeof m, "%x\n", sum);
+            log += m;
+        }
+        char head[64];
+        if (log_first || node < 0) {
+            // the very first LOG prints an empty address (the else at Log.cpp:71 binds to
+            // the sprintf at :73)
+            std::snprintf(head, sizeof head, "\n [%d] ", tick);
+        } else {
+            const int32_t id = node + 1;
+            signed char b[4];
+            std::memcpy(b, &id, 4);
+            std::snprintf(head, sizeof head, "\n %d.%d.%d.%d:%d [%d] ", b[0], b[1], b[2], b[3], 0,
+                          tick);
+        }
+        log_first = false;
+        log += head;
+        log += text;
+    }
+
+    void member_line(int32_t node, int32_t tick, int32_t subject, const char *verb) {
+        const int32_t id = subject + 1;
+        signed char b[4];
+        std::memcpy(b, &id, 4);
+        char text[96];
+        std::snprintf(text, sizeof text, "Node %d.%d.%d.%d:%d %s at time %d", b[0], b[1], b[2],
+                      b[3], 0, verb, tick);
+        append_line(node, tick, text);
+    }
+
+    int flush_log() {
+        if (!logf) return GSP_OK;
+        if (log.size() > log_flushed) {
+            std::fwrite(log.data() + log_flushed, 1, log.size() - log_flushed, logf);
+            log_flushed = log.size();
+        }
+        std::fflush(logf);
+        return GSP_OK;
+    }
+};
+
+namespace {
+
+int upload_i32(gsp::DevBuf<int32_t> &d, const std::vector<int32_t> &h, hipStream_t st) {
+    GSP_HIP(d.alloc(h.size()));
+    if (!h.empty())
+        GSP_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    return GSP_OK;
+}
+
+int check_engine(gsp_engine *e) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "engine is NULL");
+    GSP_HIP(hipSetDevice(e->device));
+    return GSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gsp_create(const gsp_params *p, int device, gsp_rng_mode rng, uint64_t seed,
+               const char *dbg_log_path, gsp_engine **out) {
+    GSP_REQUIRE(p && out, GSP_ERR_INVALID, "gsp_create: NULL argument");
+    GSP_REQUIRE(p->max_nnb >= 1 && p->max_nnb <= kMaxNodes, GSP_ERR_INVALID,
+                "gsp_create: max_nnb=%d outside [1, %d]", p->max_nnb, kMaxNodes);
+    GSP_REQUIRE(rng == GSP_RNG_GLIBC || rng == GSP_RNG_PHILOX, GSP_ERR_INVALID,
+                "gsp_create: unknown rng mode %d", int(rng));
+    *out = nullptr;
+    int ndev = 0;
+    GSP_HIP(hipGetDeviceCount(&ndev));
+    GSP_REQUIRE(device >= 0 && device < ndev, GSP_ERR_HIP, "gsp_create: device %d of %d", device,
+                ndev);
+    GSP_HIP(hipSetDevice(device));
+    std::unique_ptr<gsp_engine> e(new gsp_engine);
+    e->p = *p;
+    e->n = p->max_nnb;
+    e->device = device;
+    e->rng_mode = int(rng);
+    e->seed = seed;
+    e->glibc.reseed(uint32_t(seed));
+    const int32_t n = e->n;
+    e->queue.resize(n);
+    e->failed.assign(n, 0);
+    e->last_commit.assign(n, 0);
+    e->inited.assign(n, 0);
+    e->in_group.assign(n, 0);
+    e->own_hb.assign(n, 0);
+    e->nlist.assign(n, 0);
+    e->recv_ctr.assign(size_t(n + 1) * kMaxTicks, 0);
+    if (dbg_log_path) {
+        e->logf = std::fopen(dbg_log_path, "w");
+        GSP_REQUIRE(e->logf, GSP_ERR_IO, "gsp_create: cannot write %s", dbg_log_path);
+    }
+    GSP_HIP(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+    GSP_HIP(hipEventCreate(&e->ev0));
+    GSP_HIP(hipEventCreate(&e->ev1));
+    const size_t nn = size_t(n) * n;
+    GSP_HIP(e->t_key.alloc(nn));
+    GSP_HIP(e->t_hb.alloc(nn));
+    GSP_HIP(e->t_ts.alloc(nn));
+    GSP_HIP(e->t_rank.alloc(nn));
+    GSP_HIP(e->t_state.alloc(size_t(4) * n));
+    GSP_HIP(e->o_key.alloc(nn));
+    GSP_HIP(e->o_hb.alloc(nn));
+    GSP_HIP(e->o_ts.alloc(nn));
+    GSP_HIP(e->o_rank.alloc(nn));
+    GSP_HIP(e->o_state.alloc(size_t(4) * n));
+    GSP_HIP(e->counters.alloc(4));
+    GSP_HIP(e->merges.alloc(1));
+    GSP_HIP(e->sent_ctr.alloc(size_t(n + 1) * kMaxTicks));
+    GSP_HIP(hipMemsetAsync(e->t_key.p, 0xFF, nn * sizeof(int64_t), e->st));   // all absent
+    GSP_HIP(hipMemsetAsync(e->t_hb.p, 0, nn * sizeof(int32_t), e->st));
+    GSP_HIP(hipMemsetAsync(e->t_ts.p, 0, nn * sizeof(int32_t), e->st));
+    GSP_HIP(hipMemsetAsync(e->t_rank.p, 0xFF, nn * sizeof(int32_t), e->st));
+    GSP_HIP(hipMemsetAsync(e->t_state.p, 0, size_t(4) * n * sizeof(int32_t), e->st));
+    GSP_HIP(hipMemsetAsync(e->sent_ctr.p, 0, size_t(n + 1) * kMaxTicks * sizeof(int32_t), e->st));
+    GSP_HIP(hipMemsetAsync(e->merges.p, 0, sizeof(unsigned long long), e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    *out = e.release();
+    return GSP_OK;
+}
+
+int gsp_destroy(gsp_engine *e) {
+    if (!e) return GSP_OK;
+    (void)hipSetDevice(e->device);
+    e->flush_log();
+    if (e->logf) std::fclose(e->logf);
+    if (e->st) (void)hipStreamSynchronize(e->st);
+    for (auto *b : {&e->t_hb, &e->t_ts, &e->t_rank, &e->t_state, &e->o_hb, &e->o_ts, &e->o_rank,
+                    &e->o_state, &e->b_node, &e->b_op, &e->q_off, &e->q_src, &e->q_type,
+                    &e->send_off, &e->send_dst, &e->send_type, &e->send_cnt, &e->counters,
+                    &e->stream, &e->adm_src, &e->adm_dst, &e->adm_type, &e->sent_ctr})
+        b->release();
+    e->t_key.release();
+    e->o_key.release();
+    e->events.release();
+    e->merges.release();
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    delete e;
+    return GSP_OK;
+}
+
+int gsp_tick_recv(gsp_engine *e, int32_t tick, const int32_t *order, int32_t n) {
+    GSP_REQUIRE(e && (order || n == 0) && n >= 0, GSP_ERR_INVALID, "gsp_tick_recv: bad argument");
+    GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_tick_recv: tick %d", tick);
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t node = order[i];
+        GSP_REQUIRE(node >= 0 && node < e->n, GSP_ERR_INVALID, "gsp_tick_recv: node %d", node);
+        const int32_t id = node + 1;
+        auto &b = e->buf;
+        for (int64_t k = int64_t(b.size()) - 1; k >= 0; --k) {   // EmulNet.cpp:151-173
+            if (!addr_strcmp_equal(b[size_t(k)].dst, id)) continue;
+            e->queue[node].push_back(b[size_t(k)]);
+            b[size_t(k)] = b.back();
+            b.pop_back();
+            e->recv_ctr[size_t(id) * kMaxTicks + tick]++;
+        }
+    }
+    return GSP_OK;
+}
+
+int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const int8_t *ops,
+                     int32_t n, int32_t dropmsg) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(n >= 0 && (n == 0 || (order && ops)), GSP_ERR_INVALID,
+                "gsp_tick_process: bad argument");
+    GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_tick_process: tick %d", tick);
+    if (n == 0) return GSP_OK;
+    const int32_t N = e->n;
+    GSP_REQUIRE(n <= N, GSP_ERR_INVALID, "gsp_tick_process: batch of %d > %d nodes", n, N);
+    std::vector<int8_t> seen(N, 0);
+    std::vector<int32_t> h_node(n), h_op(n), h_qoff(n + 1, 0), h_soff(n + 1, 0);
+    std::vector<int32_t> h_qsrc, h_qtype;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t node = order[i];
+        const int32_t op = ops[i];
+        GSP_REQUIRE(node >= 0 && node < N, GSP_ERR_INVALID, "gsp_tick_process: node %d", node);
+        GSP_REQUIRE(op >= GSP_OP_START && op <= GSP_OP_OPS, GSP_ERR_INVALID,
+                    "gsp_tick_process: op %d", op);
+        GSP_REQUIRE(!seen[node], GSP_ERR_ORDER,
+                    "gsp_tick_process: node %d appears twice in one batch", node);
+        seen[node] = 1;
+        h_node[i] = node;
+        h_op[i] = op;
+        int32_t njreq = 0;
+        if (op == GSP_OP_LOOP || op == GSP_OP_CHECK) {
+            for (const NetMsg &m : e->queue[node]) {
+                if (m.type == GSP_MSG_GOSSIP) {
+                    const int32_t s = m.src - 1;
+                    // the payload is the sender's list at send time (MP1Node.cpp:357); the
+                    // device reads it from the committed table, so it must be unchanged
+                    GSP_REQUIRE(s >= 0 && s < N && e->last_commit[s] == m.send_batch,
+                                GSP_ERR_ORDER,
+                                "gsp_tick_process: GOSSIP from id %d to node %d has a stale "
+                                "payload (sender re-processed since the send)", m.src, node);
+                }
+                njreq += m.type == GSP_MSG_JOINREQ;
+                h_qsrc.push_back(m.src);
+                h_qtype.push_back(m.type);
+            }
+            GSP_REQUIRE(e->queue[node].size() < (1u << 20), GSP_ERR_CAPACITY,
+                        "gsp_tick_process: queue of node %d too long", node);
+            e->queue[node].clear();
+        }
+        h_qoff[i + 1] = int32_t(h_qsrc.size());
+        h_soff[i + 1] = h_soff[i] + njreq + 1 + N;
+    }
+    const int32_t send_cap = h_soff[n];
+    hipStream_t st = e->st;
+    if (upload_i32(e->b_node, h_node, st) || upload_i32(e->b_op, h_op, st) ||
+        upload_i32(e->q_off, h_qoff, st) || upload_i32(e->q_src, h_qsrc, st) ||
+        upload_i32(e->q_type, h_qtype, st) || upload_i32(e->send_off, h_soff, st))
+        return GSP_ERR_HIP;
+    GSP_HIP(e->send_dst.alloc(send_cap));
+    GSP_HIP(e->send_type.alloc(send_cap));
+    GSP_HIP(e->send_cnt.alloc(n));
+    GSP_HIP(e->adm_src.alloc(send_cap));
+    GSP_HIP(e->adm_dst.alloc(send_cap));
+    GSP_HIP(e->adm_type.alloc(send_cap));
+    const int32_t ev_cap = n * (2 * N + 2);
+    GSP_HIP(e->events.alloc(ev_cap));
+    GSP_HIP(hipMemsetAsync(e->counters.p, 0, 4 * sizeof(int32_t), st));
+    if (e->rng_mode == GSP_RNG_GLIBC) {
+        const int32_t *vals = e->glibc.span(e->draws, send_cap);
+        GSP_HIP(e->stream.alloc(send_cap));
+        GSP_HIP(hipMemcpyAsync(e->stream.p, vals, size_t(send_cap) * sizeof(int32_t),
+                               hipMemcpyHostToDevice, st));
+    }
+
+    gsp::ExactBatchDev b{};
+    b.n_batch = n;
+    b.node = e->b_node.p; b.op = e->b_op.p;
+    b.q_off = e->q_off.p; b.q_src = e->q_src.p; b.q_type = e->q_type.p;
+    b.send_off = e->send_off.p;
+    b.o_key = e->o_key.p; b.o_hb = e->o_hb.p; b.o_ts = e->o_ts.p; b.o_rank = e->o_rank.p;
+    b.o_state = e->o_state.p;
+    b.send_dst = e->send_dst.p; b.send_type = e->send_type.p; b.send_cnt = e->send_cnt.p;
+    b.events = e->events.p; b.ev_count = e->counters.p; b.ev_cap = ev_cap;
+    b.merges = e->merges.p;
+
+    gsp::ExactSendDev s{};
+    s.n_batch = n;
+    s.node = e->b_node.p; s.send_off = e->send_off.p; s.send_cnt = e->send_cnt.p;
+    s.send_dst = e->send_dst.p; s.send_type = e->send_type.p;
+    s.rng_mode = e->rng_mode;
+    s.glibc_stream = e->stream.p;
+    s.stream_base = e->draws;
+    s.g0 = e->draws;
+    s.seed = e->seed;
+    s.tick = tick;
+    s.dropmsg = dropmsg ? 1 : 0;
+    s.drop_thr = int32_t(e->p.msg_drop_prob * 100);          // EmulNet.cpp:91
+    s.buff_room = std::max<int32_t>(0, e->p.en_buff_size - int32_t(e->buf.size()));
+    s.size_reject = (kMsgHdrBytes + kEnMsgBytes >= e->p.max_msg_size) ? 1 : 0;
+    s.adm_src = e->adm_src.p; s.adm_dst = e->adm_dst.p; s.adm_type = e->adm_type.p;
+    s.adm_count = e->counters.p + 1;
+    s.draws = e->counters.p + 2;
+    s.sent_ctr = e->sent_ctr.p;
+    s.max_ticks = kMaxTicks;
+
+    gsp::ExactTable tab = e->table();
+    GSP_HIP(hipEventRecord(e->ev0, st));
+    GSP_HIP(gsp::launch_exact_batch(tab, b, N, tick, e->batch_seq, e->p.tremove,
+                                    e->p.id_filter_limit, st));
+    GSP_HIP(gsp::launch_exact_sends(s, st));
+    GSP_HIP(gsp::launch_exact_commit(tab, b, N, st));
+    GSP_HIP(hipEventRecord(e->ev1, st));
+
+    int32_t ctr[4];
+    GSP_HIP(hipMemcpyAsync(ctr, e->counters.p, sizeof ctr, hipMemcpyDeviceToHost, st));
+    std::vector<int32_t> o_state(size_t(n) * 4);
+    GSP_HIP(hipMemcpyAsync(o_state.data(), e->o_state.p, o_state.size() * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, st));
+    unsigned long long merges = 0;
+    GSP_HIP(hipMemcpyAsync(&merges, e->merges.p, sizeof merges, hipMemcpyDeviceToHost, st));
+    GSP_HIP(hipStreamSynchronize(st));
+    GSP_REQUIRE(ctr[0] <= ev_cap, GSP_ERR_CAPACITY, "gsp_tick_process: event buffer overflow");
+    const int32_t n_ev = ctr[0], n_adm = ctr[1], n_draw = ctr[2];
+    std::vector<gsp::ExactEvent> ev(n_ev);
+    std::vector<int32_t> a_src(n_adm), a_dst(n_adm), a_type(n_adm);
+    if (n_ev)
+        GSP_HIP(hipMemcpyAsync(ev.data(), e->events.p, size_t(n_ev) * sizeof(gsp::ExactEvent),
+                               hipMemcpyDeviceToHost, st));
+    if (n_adm) {
+        GSP_HIP(hipMemcpyAsync(a_src.data(), e->adm_src.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
+        GSP_HIP(hipMemcpyAsync(a_dst.data(), e->adm_dst.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
+        GSP_HIP(hipMemcpyAsync(a_type.data(), e->adm_type.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
+    }
+    GSP_HIP(hipStreamSynchronize(st));
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->stats.device_ms += ms;
+
+    // dbg.log lines in the reference's order: batch position (call order), then within a
+    // node the start line, join lines (queue order j, payload order p), remove lines
+    // (descending list index)
+    auto phase = [](int32_t k) { return k == gsp::kEvJoin ? 1 : (k == gsp::kEvRemove ? 2 : 0); };
+    std::sort(ev.begin(), ev.end(), [&](const gsp::ExactEvent &a, const gsp::ExactEvent &c) {
+        if (a.pos != c.pos) return a.pos < c.pos;
+        if (phase(a.kind) != phase(c.kind)) return phase(a.kind) < phase(c.kind);
+        return a.ord < c.ord;
+    });
+    for (const auto &x : ev) {
+        const int32_t node = h_node[x.pos];
+        switch (x.kind) {
+            case gsp::kEvStartGroup: e->append_line(node, tick, "Starting up group..."); break;
+            case gsp::kEvStartJoin: e->append_line(node, tick, "Trying to join..."); break;
+            case gsp::kEvJoin: e->member_line(node, tick, x.subject, "joined"); break;
+            default: e->member_line(node, tick, x.subject, "removed"); break;
+        }
+    }
+    for (int32_t k = 0; k < n_adm; ++k)
+        e->buf.push_back(NetMsg{a_src[k], a_dst[k], a_type[k], e->batch_seq});
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t node = h_node[i];
+        e->inited[node] = o_state[size_t(i) * 4 + 0];
+        e->in_group[node] = o_state[size_t(i) * 4 + 1];
+        e->own_hb[node] = o_state[size_t(i) * 4 + 2];
+        e->nlist[node] = o_state[size_t(i) * 4 + 3];
+        e->last_commit[node] = e->batch_seq;
+        if (h_op[i] == GSP_OP_START) e->failed[node] = 0;   // initThisNode, MP1Node.cpp:102
+        if (h_op[i] == GSP_OP_LOOP) e->stats.node_rounds++;
+    }
+    e->draws += n_draw;
+    e->glibc.trim(e->draws);
+    e->stats.draws = e->draws;
+    e->stats.batches++;
+    e->stats.sends_admitted += n_adm;
+    e->stats.merges = int64_t(merges);
+    e->batch_seq++;
+    return GSP_OK;
+}
+
+int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value) {
+    GSP_REQUIRE(e && value, GSP_ERR_INVALID, "gsp_rand: NULL argument");
+    if (e->rng_mode == GSP_RNG_PHILOX)
+        *value = int32_t(gsp::draw_u31(gsp::kDomainFail, e->seed, uint32_t(tick), 0, 0, 0));
+    else
+        *value = e->glibc.at(e->draws);
+    e->draws++;
+    e->glibc.trim(e->draws);
+    e->stats.draws = e->draws;
+    return GSP_OK;
+}
+
+int gsp_log(gsp_engine *e, int32_t node, int32_t tick, const char *text) {
+    GSP_REQUIRE(e && text, GSP_ERR_INVALID, "gsp_log: NULL argument");
+    GSP_REQUIRE(node < e->n, GSP_ERR_INVALID, "gsp_log: node %d", node);
+    e->append_line(node, tick, text);
+    return GSP_OK;
+}
+
+int gsp_set_failed(gsp_engine *e, int32_t node, int32_t failed) {
+    GSP_REQUIRE(e && node >= 0 && node < e->n, GSP_ERR_INVALID, "gsp_set_failed: bad node");
+    e->failed[node] = failed ? 1 : 0;
+    return GSP_OK;
+}
+
+int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out) {
+    GSP_REQUIRE(e && out && node >= 0 && node < e->n, GSP_ERR_INVALID, "gsp_get_member: bad arg");
+    out->id = node + 1;
+    out->port = 0;
+    out->inited = int8_t(e->inited[node]);
+    out->in_group = int8_t(e->in_group[node]);
+    out->failed = e->failed[node];
+    out->heartbeat = e->own_hb[node];
+    out->n_members = e->nlist[node];
+    return GSP_OK;
+}
+
+int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(node >= 0 && node < e->n && n && (buf || cap == 0), GSP_ERR_INVALID,
+                "gsp_member_list: bad argument");
+    const int32_t N = e->n;
+    std::vector<int64_t> key(N);
+    std::vector<int32_t> hb(N), ts(N), rank(N);
+    const size_t row = size_t(node) * N;
+    GSP_HIP(hipMemcpyAsync(key.data(), e->t_key.p + row, N * 8, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(hb.data(), e->t_hb.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(ts.data(), e->t_ts.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(rank.data(), e->t_rank.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    std::vector<gsp_entry> list(N);
+    int32_t cnt = 0;
+    for (int32_t x = 0; x < N; ++x) {
+        if (key[x] < 0) continue;
+        GSP_REQUIRE(rank[x] >= 0 && rank[x] < N, GSP_ERR_INVALID, "corrupt rank");
+        list[rank[x]] = gsp_entry{x + 1, 0, hb[x], ts[x]};
+        cnt++;
+    }
+    *n = cnt;
+    for (int32_t k = 0; k < cnt && k < cap; ++k) buf[k] = list[k];
+    return GSP_OK;
+}
+
+int gsp_counters(gsp_engine *e, int32_t *sent, int32_t *recv, int32_t ticks) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(ticks >= 0 && ticks <= kMaxTicks, GSP_ERR_INVALID, "gsp_counters: ticks %d", ticks);
+    const int32_t N = e->n;
+    std::vector<int32_t> dev(size_t(N + 1) * kMaxTicks);
+    GSP_HIP(hipMemcpyAsync(dev.data(), e->sent_ctr.p, dev.size() * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    for (int32_t id = 0; id <= N; ++id)
+        for (int32_t t = 0; t < ticks; ++t) {
+            if (sent) sent[size_t(id) * ticks + t] = dev[size_t(id) * kMaxTicks + t];
+            if (recv) recv[size_t(id) * ticks + t] = e->recv_ctr[size_t(id) * kMaxTicks + t];
+        }
+    return GSP_OK;
+}
+
+// EmulNet::ENcleanup's msgcount.log (EmulNet.cpp:195-216), including the node-67 layout.
+int gsp_write_msgcount(gsp_engine *e, const char *path, int32_t tick) {
+    GSP_REQUIRE(e && path, GSP_ERR_INVALID, "gsp_write_msgcount: NULL argument");
+    const int32_t N = e->n;
+    std::vector<int32_t> sent(size_t(N + 1) * tick), recv(size_t(N + 1) * tick);
+    if (int rc = gsp_counters(e, sent.data(), recv.data(), tick)) return rc;
+    FILE *f = std::fopen(path, "w");
+    GSP_REQUIRE(f, GSP_ERR_IO, "gsp_write_msgcount: cannot write %s", path);
+    for (int32_t id = 1; id <= N; ++id) {
+        std::fprintf(f, "node %3d ", id);
+        uint32_t st = 0, rt = 0;
+        for (int32_t j = 0; j < tick; ++j) {
+            const int32_t a = sent[size_t(id) * tick + j], c = recv[size_t(id) * tick + j];
+            st += uint32_t(a);
+            rt += uint32_t(c);
+            if (id == 67) {
+                std::fprintf(f, "special %4d %4d %4d\n", j, a, c);
+            } else {
+                std::fprintf(f, " (%4d, %4d)", a, c);
+                if (j % 10 == 9) std::fprintf(f, "\n         ");
+            }
+        }
+        std::fprintf(f, "\nnode %3d sent_total %6u  recv_total %6u\n\n", id, st, rt);
+    }
+    std::fclose(f);
+    return GSP_OK;
+}
+
+int gsp_flush_log(gsp_engine *e) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "gsp_flush_log: NULL engine");
+    return e->flush_log();
+}
+
+int gsp_log_bytes(gsp_engine *e, char *buf, size_t cap, size_t *n) {
+    GSP_REQUIRE(e && n, GSP_ERR_INVALID, "gsp_log_bytes: NULL argument");
+    *n = e->log.size();
+    if (buf && cap) std::memcpy(buf, e->log.data(), std::min(cap, e->log.size()));
+    return GSP_OK;
+}
+
+int gsp_exact_stats_get(gsp_engine *e, gsp_exact_stats *out) {
+    GSP_REQUIRE(e && out, GSP_ERR_INVALID, "gsp_exact_stats_get: NULL argument");
+    *out = e->stats;
+    return GSP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,91 @@
+"""Python side of the SCALE engine (gsp_scale_* in include/gossip/gossip.h).
+
+Entries come back packed as the device stores them: hb << 5 | (ts mod 32), 0 = absent.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+FAIL_NONE, FAIL_RANDOM, FAIL_BLOCK = 0, 1, 2
+
+
+def unpack(entries):
+    e = np.asarray(entries, dtype=np.uint16)
+    present = e != 0
+    return present, (e >> 5).astype(np.int32), (e & 31).astype(np.int32)
+
+
+class ScaleEngine:
+    def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
+                 fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0):
+        self.params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
+                                          h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
+                                          fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
+        self._h = ctypes.c_void_p()
+        check(lib().gsp_scale_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
+              "gsp_scale_create")
+        self.n = n
+        self.fanout = fanout
+
+    def close(self):
+        if self._h:
+            check(lib().gsp_scale_destroy(self._h), "gsp_scale_destroy")
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def step(self, ticks=1):
+        check(lib().gsp_scale_step(self._h, ticks), "gsp_scale_step")
+
+    def sync(self):
+        check(lib().gsp_scale_sync(self._h), "gsp_scale_sync")
+
+    @property
+    def tick(self):
+        t = ctypes.c_int32()
+        check(lib().gsp_scale_tick(self._h, ctypes.byref(t)), "gsp_scale_tick")
+        return t.value
+
+    def digest(self, t):
+        d = _lib.GspScaleDigest()
+        check(lib().gsp_scale_digest_get(self._h, t, ctypes.byref(d)), "gsp_scale_digest_get")
+        return {k: getattr(d, k) for k, _ in d._fields_}
+
+    def row(self, r):
+        buf = np.zeros(self.n, np.uint16)
+        check(lib().gsp_scale_row(self._h, r, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint16)),
+                                  self.n), "gsp_scale_row")
+        return buf
+
+    def own_hb(self, r):
+        v = ctypes.c_int32()
+        check(lib().gsp_scale_own_hb(self._h, r, ctypes.byref(v)), "gsp_scale_own_hb")
+        return v.value
+
+    def messages(self):
+        n = ctypes.c_int64()
+        check(lib().gsp_scale_messages(self._h, None, 0, ctypes.byref(n)), "gsp_scale_messages")
+        buf = np.zeros(max(n.value, 1), np.int32)
+        check(lib().gsp_scale_messages(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       n.value, ctypes.byref(n)), "gsp_scale_messages")
+        return buf[:n.value].reshape(-1, self.fanout)
+
+    def perf(self):
+        p = _lib.GspScalePerf()
+        check(lib().gsp_scale_perf_get(self._h, ctypes.byref(p)), "gsp_scale_perf_get")
+        return {k: getattr(p, k) for k, _ in p._fields_}
+
+    def set_timing(self, on):
+        check(lib().gsp_scale_set_timing(self._h, int(on)), "gsp_scale_set_timing")
+
+    def stream(self):
+        s = ctypes.c_void_p()
+        check(lib().gsp_scale_hip_stream(self._h, ctypes.byref(s)), "gsp_scale_hip_stream")
+        return s.value

@@ -1,0 +1,231 @@
+/*
+ * include/gossip/gossip.h -- the drop-in boundary of the MI355X gossip-membership engine.
+ *
+ * Plain C ABI (extern "C", plain pointers and sizes, int status returns, no exceptions
+ * and no torch/HIP types) over libgossip_amd.so.  Two engines live behind it:
+ *
+ *  gsp_engine  -- EXACT mode: the reference MP1 semantics, bit-exact.  The caller drives
+ *                 it with the same per-tick call pattern the reference Application uses
+ *                 on MP1Node/EmulNet (/root/reference/Application.cpp:121-202); the
+ *                 engine batches the calls of one phase and runs them as HIP kernels
+ *                 (merge = MP1Node::recvCallBack, ops = MP1Node::nodeLoopOps).  The C++
+ *                 facade in <gossip/mp1_facade.hpp> keeps the reference's class and method
+ *                 names on top of these entry points.
+ *  gsp_scale   -- SCALE mode: the build-defined full-view protocol with the
+ *                 membership table resident in HBM as packed 16-bit entries and one fused
+ *                 HIP kernel per tick; rows sharded over GPUs.
+ *
+ * Every entry point returns GSP_OK (0) or a negative gsp_status.  gsp_last_error()
+ * returns a human-readable message for the last failure on the calling thread.
+ * Threading: an engine is used by one host thread at a time.  Ownership: the engine
+ * owns all device and pinned memory; callers own every buffer they pass in.
+ */
+#ifndef GOSSIP_GOSSIP_H
+#define GOSSIP_GOSSIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSP_ABI_VERSION 1
+
+typedef enum {
+    GSP_OK = 0,
+    GSP_ERR_INVALID = -1,      /* bad argument                                       */
+    GSP_ERR_IO = -2,           /* file could not be read / written                   */
+    GSP_ERR_HIP = -3,          /* a HIP runtime call failed (no GPU, OOM, fault)      */
+    GSP_ERR_ORDER = -4,        /* call order the batched engine cannot reproduce     */
+    GSP_ERR_CAPACITY = -5,     /* a device buffer bound was exceeded                  */
+    GSP_ERR_RCCL = -6,         /* an RCCL call failed                                  */
+    GSP_ERR_RANGE = -7         /* a value would overflow its packed representation   */
+} gsp_status;
+
+const char *gsp_last_error(void);
+int gsp_abi_version(void);
+/* Number of visible HIP devices (0 when none); never fails. */
+int gsp_device_count(void);
+
+/* ------------------------------------------------------------------------------------
+ * Replay draws.  The counter-based Philox4x32-10 the engine uses in GSP_RNG_PHILOX mode,
+ * host-callable so that the reference-side EmulNet replay hook can make
+ * the identical draw in place of rand() at EmulNet.cpp:89 and Application.cpp:182/189:
+ *   drop draw:  gsp_replay_draw(GSP_DOMAIN_SEND, seed, tick, src_id, dst_id, msgType)
+ *   fail draw:  gsp_replay_draw(GSP_DOMAIN_FAIL, seed, tick, 0, 0, 0)
+ * The value is in [0, 2^31) like rand().
+ * ---------------------------------------------------------------------------------- */
+#define GSP_DOMAIN_SEND 0x53454E44u
+#define GSP_DOMAIN_FAIL 0x4641494Cu
+#define GSP_DOMAIN_PEER 0x50454552u
+uint32_t gsp_replay_draw(uint32_t domain, uint64_t seed, uint32_t a, uint32_t b, uint32_t c,
+                         uint32_t d);
+int gsp_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+/* ------------------------------------------------------------------------------------
+ * Params -- /root/reference/Params.{h,cpp}.  gsp_params_from_conf parses the same
+ * four-key .conf grammar as Params::setparams (Params.cpp:19-43) and fills the same
+ * hard-coded values (STEP_RATE 0.25, MAX_MSG_SIZE 4000, Params.cpp:29-31).
+ * ---------------------------------------------------------------------------------- */
+typedef struct {
+    int32_t max_nnb;            /* MAX_NNB -> EN_GPSZ, the number of peers             */
+    int32_t single_failure;     /* SINGLE_FAILURE                                      */
+    int32_t drop_msg;           /* DROP_MSG                                            */
+    double msg_drop_prob;       /* MSG_DROP_PROB                                       */
+    double step_rate;           /* STEP_RATE (join schedule), 0.25                      */
+    int32_t max_msg_size;       /* MAX_MSG_SIZE, 4000                                  */
+    int32_t en_buff_size;       /* EmulNet buffer bound, ENBUFFSIZE 30000 (EmulNet.h:12) */
+    int32_t total_running_time; /* TOTAL_RUNNING_TIME, 700 (Application.h:27)          */
+    int32_t tremove;            /* TREMOVE, 20 (MP1Node.h:21)                          */
+    int32_t id_filter_limit;    /* payload filter id < limit, 10 (MP1Node.cpp:245)     */
+} gsp_params;
+
+int gsp_params_default(gsp_params *out);
+int gsp_params_from_conf(const char *path, gsp_params *out);
+
+/* ------------------------------------------------------------------------------------
+ * EXACT engine
+ * ---------------------------------------------------------------------------------- */
+typedef struct gsp_engine gsp_engine;
+
+typedef enum {
+    GSP_RNG_GLIBC = 0,  /* the reference's srand(seed)/rand() stream, indexed by draw order */
+    GSP_RNG_PHILOX = 1  /* counter-based replay: Philox4x32-10(seed; tick, src, dst, type)  */
+} gsp_rng_mode;
+
+typedef enum {          /* message types, /root/reference/MP1Node.h:31-36 */
+    GSP_MSG_JOINREQ = 0,
+    GSP_MSG_JOINREP = 1,
+    GSP_MSG_GOSSIP = 3
+} gsp_msg_type;
+
+typedef enum {          /* per-node operations of one phase-P batch */
+    GSP_OP_START = 0,   /* MP1Node::nodeStart     (MP1Node.cpp:67)                     */
+    GSP_OP_LOOP = 1,    /* MP1Node::nodeLoop      (MP1Node.cpp:176): drain + ops if inGroup */
+    GSP_OP_CHECK = 2,   /* MP1Node::checkMessages (MP1Node.cpp:200): drain only         */
+    GSP_OP_OPS = 3      /* MP1Node::nodeLoopOps   (MP1Node.cpp:335)                      */
+} gsp_op;
+
+/* Create an engine for p->max_nnb nodes (<= 1024) on HIP device `device`.
+ * dbg_log_path: where the dbg.log event stream is written (NULL: keep in memory only).
+ * The engine assigns node i the address id i+1, port 0 (EmulNet::ENinit, EmulNet.cpp:72). */
+int gsp_create(const gsp_params *p, int device, gsp_rng_mode rng, uint64_t seed,
+               const char *dbg_log_path, gsp_engine **out);
+int gsp_destroy(gsp_engine *e);
+
+/* Phase R: EmulNet::ENrecv for each node in `order`, in that order (the reference calls
+ * MP1Node::recvLoop for i ascending, Application.cpp:125-135).  Delivery follows the
+ * reference buffer permutation (top-down scan, swap-with-last, EmulNet.cpp:151-161). */
+int gsp_tick_recv(gsp_engine *e, int32_t tick, const int32_t *order, int32_t n);
+
+/* Phase P: one batch of per-node operations, executed in `order` (the reference calls
+ * them for i descending, Application.cpp:138-163).  dropmsg is Params::dropmsg at call
+ * time.  A node may appear at most once per batch. */
+int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const int8_t *ops,
+                     int32_t n, int32_t dropmsg);
+
+/* One rand() draw in the engine's global draw order (the draw Application::fail makes,
+ * Application.cpp:182/189).  In Philox mode the draw is Philox(seed; tick, 0, 0, 0). */
+int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value);
+
+/* A line from the driver into dbg.log, ordered after all work submitted before it
+ * (Log::LOG, Log.cpp:44).  node < 0 prints the empty address of the very first LOG. */
+int gsp_log(gsp_engine *e, int32_t node, int32_t tick, const char *text);
+
+/* Member mirror (/root/reference/Member.h:89-122). */
+typedef struct {
+    int32_t id;
+    int16_t port;
+    int8_t inited, in_group, failed;
+    int64_t heartbeat;
+    int32_t n_members;
+} gsp_member_view;
+typedef struct {
+    int32_t id;
+    int16_t port;
+    int64_t heartbeat;
+    int64_t timestamp;
+} gsp_entry;
+int gsp_set_failed(gsp_engine *e, int32_t node, int32_t failed);
+int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out);
+/* The member list of `node` in list order (MemberListEntry vector order). */
+int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n);
+
+/* EmulNet::ENcleanup (EmulNet.cpp:184-220): writes msgcount.log for ticks [0, tick). */
+int gsp_write_msgcount(gsp_engine *e, const char *path, int32_t tick);
+/* Per-(node, tick) counters: sent[(id) * ticks + t], recv likewise, id in 1..N. */
+int gsp_counters(gsp_engine *e, int32_t *sent, int32_t *recv, int32_t ticks);
+/* Flush buffered dbg.log bytes to disk (done automatically on destroy). */
+int gsp_flush_log(gsp_engine *e);
+/* Copy the whole dbg.log byte stream produced so far. *n receives the full size. */
+int gsp_log_bytes(gsp_engine *e, char *buf, size_t cap, size_t *n);
+
+typedef struct {
+    int64_t batches;            /* phase-P batches executed on the device             */
+    int64_t node_rounds;        /* GSP_OP_LOOP operations executed                      */
+    int64_t merges;             /* member-entry merges: 1 + |payload| per GOSSIP        */
+    int64_t draws;              /* rand() draws consumed                                */
+    int64_t sends_admitted;     /* messages appended to the EmulNet buffer             */
+    double device_ms;           /* time inside the exact-mode kernels (HIP events)     */
+} gsp_exact_stats;
+int gsp_exact_stats_get(gsp_engine *e, gsp_exact_stats *out);
+
+/* ------------------------------------------------------------------------------------
+ * SCALE engine (full view, packed entries, device-resident tick loop)
+ * ---------------------------------------------------------------------------------- */
+typedef struct gsp_scale gsp_scale;
+
+typedef struct {
+    int32_t n;          /* nodes; full view V = n                                     */
+    int32_t fanout;     /* peers per sender per tick (distinct), 1..16                 */
+    int32_t drop_pct;   /* a send is dropped iff Philox % 100 < drop_pct               */
+    int32_t tremove;    /* TREMOVE (20)                                                */
+    int32_t h0;         /* initial heartbeat of every pre-joined entry (>= 1)          */
+    int32_t fail_mode;  /* 0 none, 1 per-node Bernoulli(fail_ppm), 2 contiguous block  */
+    int32_t fail_tick;  /* failed nodes stop after this tick                           */
+    int32_t fail_ppm;   /* failure fraction in parts per million                       */
+    uint64_t seed;
+    int32_t max_ticks;  /* bound for digest storage; hb must stay <= 2047 (h0+ticks)   */
+} gsp_scale_params;
+
+typedef struct {
+    int64_t tick, node_rounds, merges, sent, dropped, delivered, joins, removes;
+    uint64_t event_hash;   /* sum over events of mix64(kind, t, r, x), order independent */
+} gsp_scale_digest;
+
+typedef struct {
+    int64_t ticks;            /* ticks stepped                                        */
+    int64_t merge_launches;   /* fused tick-kernel launches timed                     */
+    double merge_ms;          /* sum of fused tick-kernel durations (HIP events)      */
+    double csr_ms;            /* sum of CSR build kernel durations                    */
+    double bytes_per_tick;    /* algorithmic HBM bytes of the fused kernel, last tick  */
+} gsp_scale_perf;
+
+/* Single-GPU engine on `device` (rows [0, n)). */
+int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out);
+int gsp_scale_destroy(gsp_scale *s);
+/* Advance `ticks` ticks on the device (no host synchronisation inside). */
+int gsp_scale_step(gsp_scale *s, int32_t ticks);
+/* Wait for all submitted work. */
+int gsp_scale_sync(gsp_scale *s);
+/* Current tick (last completed). */
+int gsp_scale_tick(gsp_scale *s, int32_t *tick);
+/* Digest of tick t (1 <= t <= current tick). */
+int gsp_scale_digest_get(gsp_scale *s, int32_t t, gsp_scale_digest *out);
+/* Row r of the current table, packed entries (hb << 5 | ts mod 32; 0 = absent). */
+int gsp_scale_row(gsp_scale *s, int32_t r, uint16_t *buf, int32_t cap);
+int gsp_scale_own_hb(gsp_scale *s, int32_t r, int32_t *hb);
+/* Surviving messages sent at the current tick: dst per (src, k) slot, -1 = none/dropped. */
+int gsp_scale_messages(gsp_scale *s, int32_t *dst, int64_t cap, int64_t *n);
+int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out);
+/* Enable/disable per-launch HIP event timing (default on). */
+int gsp_scale_set_timing(gsp_scale *s, int32_t on);
+/* The hipStream_t (as void*) every launch of this engine is ordered on, so a caller can
+ * bracket a timed region with its own HIP events on the same stream. */
+int gsp_scale_hip_stream(gsp_scale *s, void **stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOSSIP_GOSSIP_H */

@@ -243,3 +243,12 @@ int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32
     if (dst) memcpy(dst, o->mdst, sizeof(int32_t) * k);
     return o->nmsg;
 }
+
+/* exported for the known-answer tests */
+void gsp_oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    gsp_philox4x32_10(ctr, key, out);
+}
+uint32_t gsp_oracle_draw(uint32_t domain, uint64_t seed, uint32_t a, uint32_t b, uint32_t c,
+                         uint32_t d) {
+    return gsp_philox_u31(domain, seed, a, b, c, d);
+}

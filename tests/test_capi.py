@@ -1,0 +1,96 @@
+"""The C-ABI boundary (CPU only: no compute calls that need a GPU).
+
+* libgossip_amd.so loads and exports every function include/gossip/gossip.h declares;
+* the ctypes stub (gossip_protocol_amd/_lib.py) covers every declared function;
+* Params parsing follows Params::setparams (Params.cpp:19-43);
+* the host-side replay draw is the oracle's Philox, and matches Random123's KATs;
+* without a GPU the engine constructors fail loudly (no silent CPU fallback).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+from gossip_protocol_amd import _lib
+from tests.oracle_binding import GOLDEN, load_oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for hdr in ["include/gossip/gossip.h"]:
+        src = open(os.path.join(ROOT, hdr)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^[a-z_A-Z][\w \*]*?\b(gsp_\w+)\s*\(", src, flags=re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ["gsp_create", "gsp_tick_recv", "gsp_tick_process", "gsp_scale_create",
+                 "gsp_scale_step", "gsp_params_from_conf", "gsp_replay_draw"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_ctypes_stub_covers_header():
+    missing = [n for n in declared_functions() if n not in _lib.SIGNATURES]
+    assert not missing, missing
+    _lib.lib()  # every signature binds
+
+
+def test_params_from_conf():
+    L = _lib.lib()
+    for conf, want in [("singlefailure", (10, 1, 0)), ("multifailure", (10, 0, 0)),
+                       ("msgdropsinglefailure", (10, 1, 1))]:
+        p = _lib.GspParams()
+        rc = L.gsp_params_from_conf(os.path.join(GOLDEN, "testcases", conf + ".conf").encode(),
+                                    ctypes.byref(p))
+        assert rc == 0
+        assert (p.max_nnb, p.single_failure, p.drop_msg) == want
+        assert abs(p.msg_drop_prob - 0.1) < 1e-12
+        assert p.step_rate == 0.25 and p.max_msg_size == 4000 and p.tremove == 20
+    p = _lib.GspParams()
+    assert L.gsp_params_from_conf(b"/nonexistent.conf", ctypes.byref(p)) == -2
+    assert b"cannot open" in L.gsp_last_error()
+
+
+def test_replay_draw_matches_oracle():
+    L = _lib.lib()
+    O = load_oracle()
+    O.gsp_oracle_draw.restype = ctypes.c_uint32
+    O.gsp_oracle_draw.argtypes = [ctypes.c_uint32, ctypes.c_uint64] + [ctypes.c_uint32] * 4
+    for dom in [0x53454E44, 0x4641494C, 0x50454552]:
+        for seed in [0, 1, 10, 0x5EED, 2**40 + 7]:
+            for a in range(0, 700, 97):
+                args = (dom, seed, a, 3, 7, 3)
+                assert L.gsp_replay_draw(*args) == O.gsp_oracle_draw(*args)
+
+
+def test_product_philox_known_answer():
+    L = _lib.lib()
+    c = (ctypes.c_uint32 * 4)(0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344)
+    k = (ctypes.c_uint32 * 2)(0xa4093822, 0x299f31d0)
+    o = (ctypes.c_uint32 * 4)()
+    assert L.gsp_philox4x32_10(c, k, o) == 0
+    assert tuple(o) == (0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1)
+
+
+def test_no_gpu_fails_loudly():
+    L = _lib.lib()
+    if L.gsp_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    p = _lib.GspParams()
+    L.gsp_params_default(ctypes.byref(p))
+    h = ctypes.c_void_p()
+    assert L.gsp_create(ctypes.byref(p), 0, 0, 1, None, ctypes.byref(h)) != 0
+    sp = _lib.GspScaleParams(n=1024, fanout=3, tremove=20, h0=1, max_ticks=16)
+    assert L.gsp_scale_create(ctypes.byref(sp), 0, ctypes.byref(h)) != 0

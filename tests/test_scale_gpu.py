@@ -1,0 +1,111 @@
+"""SCALE mode on the GPU against the scale-protocol oracle (oracle/scale_oracle.c).
+
+Small n (the oracle finishes in seconds): every tick's digest (node-rounds, merges, sends,
+drops, deliveries, join/remove counts, order-independent event hash) must be identical,
+the message lists identical, and full membership state identical: presence and heartbeat
+exactly, timestamps modulo 32 (the device's packed representation; DESIGN.md proves every
+comparison the protocol makes is exact under it).
+"""
+import numpy as np
+import pytest
+
+from gossip_protocol_amd.scale import FAIL_BLOCK, FAIL_NONE, FAIL_RANDOM, ScaleEngine, unpack
+from tests.oracle_binding import ScaleOracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # n, fanout, drop_pct, fail_mode, fail_tick, fail_ppm, seed, ticks
+    (64, 3, 0, FAIL_NONE, 10, 0, 1, 40),
+    (300, 3, 10, FAIL_RANDOM, 10, 50000, 7, 45),
+    (2048, 3, 0, FAIL_RANDOM, 10, 10000, 0x5EED, 40),
+    (2100, 5, 10, FAIL_BLOCK, 8, 50000, 99, 36),      # ragged: n not a multiple of 2048
+    (4096, 1, 30, FAIL_RANDOM, 5, 20000, 3, 30),
+]
+
+
+def _compare_state(eng, orc, n, rows):
+    for r in rows:
+        pres_o, hb_o, ts_o = orc.row(r)
+        pres_d, hb_d, ts5_d = unpack(eng.row(r))
+        assert np.array_equal(pres_d, pres_o.astype(bool)), "presence row %d" % r
+        assert np.array_equal(hb_d[pres_d], hb_o[pres_d]), "hb row %d" % r
+        assert np.array_equal(ts5_d[pres_d], ts_o[pres_d] & 31), "ts row %d" % r
+        if orc.fail_tick(r) >= eng.tick:
+            assert eng.own_hb(r) == orc.own_hb(r), "own hb row %d" % r
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_f%d_d%d_m%d" % c[:4])
+def test_scale_matches_oracle(case):
+    n, f, drop, mode, ftick, ppm, seed, ticks = case
+    orc = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                      seed=seed)
+    rng = np.random.default_rng(seed)
+    with ScaleEngine(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                     seed=seed, max_ticks=ticks) as eng:
+        # tick-0 sends (pre-joined bootstrap)
+        src, dst = orc.messages()
+        m = eng.messages()
+        got = sorted((s, d) for s in range(n) for d in m[s] if d >= 0)
+        assert got == sorted(zip(src.tolist(), dst.tolist()))
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            got = eng.digest(t)
+            assert got == want, "tick %d digest\n got %s\nwant %s" % (t, got, want)
+            if t % 7 == 0 or t in (1, ftick + 1, ftick + 21, ticks):
+                src, dst = orc.messages()
+                m = eng.messages()
+                gm = sorted((s, d) for s in range(n) for d in m[s] if d >= 0)
+                assert gm == sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+                rows = sorted(set(rng.integers(0, n, 24).tolist()) | {0, n - 1})
+                _compare_state(eng, orc, n, rows)
+        _compare_state(eng, orc, n, range(n) if n <= 512 else range(0, n, 61))
+        perf = eng.perf()
+        assert perf["ticks"] == ticks and perf["merge_ms"] > 0
+
+
+def test_scale_full_size_properties():
+    """BASELINE config 3 size (65,536 full view): size-independent properties.
+
+    * conservation: delivered + lost-to-crashed = sent - dropped of the previous tick;
+    * node-rounds equal the alive count; merges = delivered + sum of sender list sizes;
+    * a sampled row recomputed on the host from the previous tick's rows and the message
+      list equals the device's row (checks the fused kernel at full size).
+    """
+    n = 65536
+    with ScaleEngine(n, fanout=3, drop_pct=0, fail_mode=FAIL_RANDOM, fail_tick=10,
+                     fail_ppm=10000, seed=0x5EED, max_ticks=40) as eng:
+        eng.step(12)
+        d11, d12 = eng.digest(11), eng.digest(12)
+        alive = d12["node_rounds"]
+        assert 0.985 * n < alive < 0.995 * n
+        assert d11["node_rounds"] == n
+        assert d12["delivered"] <= d11["sent"] - d11["dropped"]
+        assert d12["merges"] >= d12["delivered"]
+        # host recompute of a few rows for tick 13
+        msgs = eng.messages()           # sent at tick 12, delivered at 13
+        rows_prev = {}
+        targets = [5, 4097, n - 3]
+        senders = {}
+        for s in range(n):
+            for dd in msgs[s]:
+                if dd in targets:
+                    senders.setdefault(int(dd), []).append(s)
+        need = set(targets) | {s for v in senders.values() for s in v}
+        for r in need:
+            rows_prev[r] = eng.row(r).astype(np.uint32)
+        eng.step(1)
+        t5, tr = 13 & 31, 20
+        for r in targets:
+            e = rows_prev[r].copy()
+            for s in sorted(senders.get(r, [])):
+                v = rows_prev[s]
+                he, hv = e >> 5, v >> 5
+                upd = np.where(hv > he, (v & 0xFFE0) | t5, e)
+                add = np.where((v != 0) & (((t5 - v) & 31) < tr), v, 0)
+                e = np.where(e != 0, upd, add)
+                e[s] = (((e[s] >> 5) + 1) << 5) | t5
+            e[r] = 0
+            e = np.where((e != 0) & (((t5 - e) & 31) >= tr), 0, e)
+            assert np.array_equal(e.astype(np.uint16), eng.row(r)), "row %d" % r
