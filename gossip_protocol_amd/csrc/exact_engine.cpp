@@ -66,6 +66,7 @@ struct gsp_engine {
     std::vector<int64_t> last_commit;
     std::vector<int32_t> inited, in_group, own_hb, nlist;
     std::vector<int32_t> recv_ctr;            // [(n+1) * kMaxTicks]
+    std::vector<int32_t> sent_host;           // sends issued through gsp_send
 
     // dbg.log
     std::string log;
@@ -188,6 +189,7 @@ int gsp_create(const gsp_params *p, int device, gsp_rng_mode rng, uint64_t seed,
     e->own_hb.assign(n, 0);
     e->nlist.assign(n, 0);
     e->recv_ctr.assign(size_t(n + 1) * kMaxTicks, 0);
+    e->sent_host.assign(size_t(n + 1) * kMaxTicks, 0);
     if (dbg_log_path) {
         e->logf = std::fopen(dbg_log_path, "w");
         GSP_REQUIRE(e->logf, GSP_ERR_IO, "gsp_create: cannot write %s", dbg_log_path);
@@ -433,6 +435,36 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     return GSP_OK;
 }
 
+int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
+             int32_t dropmsg, int32_t *admitted) {
+    GSP_REQUIRE(e && admitted, GSP_ERR_INVALID, "gsp_send: NULL argument");
+    GSP_REQUIRE(src_node >= 0 && src_node < e->n, GSP_ERR_INVALID, "gsp_send: node %d", src_node);
+    GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_send: tick %d", tick);
+    GSP_REQUIRE(type == GSP_MSG_JOINREQ || type == GSP_MSG_JOINREP || type == GSP_MSG_GOSSIP,
+                GSP_ERR_INVALID, "gsp_send: type %d", type);
+    const int32_t src_id = src_node + 1;
+    int32_t draw;                                            // EmulNet.cpp:89, always drawn
+    if (e->rng_mode == GSP_RNG_PHILOX)
+        draw = int32_t(gsp::draw_u31(gsp::kDomainSend, e->seed, uint32_t(tick), uint32_t(src_id),
+                                     uint32_t(dst_id), uint32_t(type)));
+    else
+        draw = e->glibc.at(e->draws);
+    e->draws++;
+    e->glibc.trim(e->draws);
+    e->stats.draws = e->draws;
+    const int32_t thr = int32_t(e->p.msg_drop_prob * 100);
+    *admitted = 0;
+    if (int32_t(e->buf.size()) >= e->p.en_buff_size ||
+        kMsgHdrBytes + kEnMsgBytes >= e->p.max_msg_size || (dropmsg && draw % 100 < thr))
+        return GSP_OK;
+    // the payload of a GOSSIP is the sender's list as committed now
+    e->buf.push_back(NetMsg{src_id, dst_id, type, e->last_commit[src_node]});
+    e->sent_host[size_t(src_id) * kMaxTicks + tick]++;
+    e->stats.sends_admitted++;
+    *admitted = kMsgHdrBytes;
+    return GSP_OK;
+}
+
 int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value) {
     GSP_REQUIRE(e && value, GSP_ERR_INVALID, "gsp_rand: NULL argument");
     if (e->rng_mode == GSP_RNG_PHILOX)
@@ -505,7 +537,9 @@ int gsp_counters(gsp_engine *e, int32_t *sent, int32_t *recv, int32_t ticks) {
     GSP_HIP(hipStreamSynchronize(e->st));
     for (int32_t id = 0; id <= N; ++id)
         for (int32_t t = 0; t < ticks; ++t) {
-            if (sent) sent[size_t(id) * ticks + t] = dev[size_t(id) * kMaxTicks + t];
+            if (sent)
+                sent[size_t(id) * ticks + t] = dev[size_t(id) * kMaxTicks + t] +
+                                               e->sent_host[size_t(id) * kMaxTicks + t];
             if (recv) recv[size_t(id) * ticks + t] = e->recv_ctr[size_t(id) * kMaxTicks + t];
         }
     return GSP_OK;

@@ -125,6 +125,12 @@ int gsp_tick_recv(gsp_engine *e, int32_t tick, const int32_t *order, int32_t n);
 int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const int8_t *ops,
                      int32_t n, int32_t dropmsg);
 
+/* EmulNet::ENsend issued directly by the caller (EmulNet.cpp:87-118): one draw, the drop
+ * window and buffer bound, then the message joins the buffer.  A GOSSIP's payload is the
+ * sender's current member list.  Returns GSP_OK; *admitted = message size or 0. */
+int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
+             int32_t dropmsg, int32_t *admitted);
+
 /* One rand() draw in the engine's global draw order (the draw Application::fail makes,
  * Application.cpp:182/189).  In Philox mode the draw is Philox(seed; tick, 0, 0, 0). */
 int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value);
