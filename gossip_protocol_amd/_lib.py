@@ -74,6 +74,8 @@ SIGNATURES = {
     "gsp_tick_recv": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32), c_int32]),
     "gsp_tick_process": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32), P(ctypes.c_int8),
                                         c_int32, c_int32]),
+    "gsp_send": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                P(c_int32)]),
     "gsp_rand": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
     "gsp_log": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, ctypes.c_char_p]),
     "gsp_set_failed": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32]),
@@ -97,6 +99,7 @@ SIGNATURES = {
     "gsp_scale_messages": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int64, P(c_int64)]),
     "gsp_scale_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
     "gsp_scale_set_timing": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_scale_set_cache_policy": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
     "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
 }
 

@@ -7,6 +7,7 @@
 //   scale_tick_kernel            merge + ops + events + send, one workgroup per row
 // The membership table lives in HBM as two [rows][stride] uint16 buffers (tick parity).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -24,7 +25,8 @@ struct gsp_scale {
     int32_t tick = 0;
     bool timing = true;
     gsp::DevBuf<uint16_t> table[2];
-    gsp::DevBuf<int32_t> own_hb, fail_tick, cnt[2], out_dst, deg, off, fill, csr_src, err;
+    gsp::DevBuf<int32_t> own_hb, fail_tick, cnt[2], out_dst, deg, off, fill, csr_src, err, tile_sum;
+    int policy = 0;   // cache policy of the row streams (scale_kernels.hpp)
     gsp::DevBuf<unsigned long long> dig;
     std::vector<int32_t> h_fail;
     struct Timed { hipEvent_t a, b, c; };
@@ -126,6 +128,7 @@ int scale_alloc(gsp_scale *s) {
     GSP_HIP(s->fill.alloc(size_t(n)));
     GSP_HIP(s->csr_src.alloc(size_t(n) * s->p.fanout));
     GSP_HIP(s->err.alloc(1));
+    GSP_HIP(s->tile_sum.alloc(size_t(n) / 4096 + 1));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(s->dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(s->dig.p, 0, dig * sizeof(unsigned long long), s->st));
@@ -183,6 +186,7 @@ int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out) {
     s->rows = p->n;
     s->row0 = 0;
     s->h_fail = gsp::scale_fail_ticks(*p);
+    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 3;
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
     if (int rc = scale_alloc(s.get())) return rc;
     const size_t lds = gsp::scale_lds_bytes(s->stride);
@@ -209,7 +213,7 @@ int gsp_scale_destroy(gsp_scale *s) {
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
     for (int b = 0; b < 2; ++b) { s->table[b].release(); s->cnt[b].release(); }
     for (auto *b : {&s->own_hb, &s->fail_tick, &s->out_dst, &s->deg, &s->off, &s->fill,
-                    &s->csr_src, &s->err})
+                    &s->csr_src, &s->err, &s->tile_sum})
         b->release();
     s->dig.release();
     if (s->st) (void)hipStreamDestroy(s->st);
@@ -231,13 +235,13 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
             tm = {s->event(), s->event(), s->event()};
             GSP_HIP(hipEventRecord(tm.a, s->st));
         }
-        GSP_HIP(gsp::launch_exclusive_scan(s->deg.p, s->off.p, n, s->st));
+        GSP_HIP(gsp::launch_exclusive_scan(s->deg.p, s->off.p, n, s->tile_sum.p, s->st));
         GSP_HIP(hipMemsetAsync(s->fill.p, 0, size_t(n) * 4, s->st));
         GSP_HIP(gsp::launch_scatter(s->out_dst.p, slots, s->p.fanout, s->row0, s->off.p, s->fill.p,
                                     s->csr_src.p, s->st));
         GSP_HIP(hipMemsetAsync(s->deg.p, 0, size_t(n) * 4, s->st));
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
-        GSP_HIP(gsp::launch_scale_tick(s->args(t), s->st));
+        GSP_HIP(gsp::launch_scale_tick(s->args(t), s->policy, s->st));
         if (s->timing) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);
@@ -334,6 +338,13 @@ int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out) {
 int gsp_scale_set_timing(gsp_scale *s, int32_t on) {
     GSP_REQUIRE(s, GSP_ERR_INVALID, "gsp_scale_set_timing: NULL");
     s->timing = on != 0;
+    return GSP_OK;
+}
+
+int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy) {
+    GSP_REQUIRE(s && policy >= 0 && policy <= 3, GSP_ERR_INVALID,
+                "gsp_scale_set_cache_policy: policy %d", policy);
+    s->policy = policy;
     return GSP_OK;
 }
 

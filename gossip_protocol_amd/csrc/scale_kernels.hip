@@ -59,14 +59,34 @@ __device__ inline void patch16(uint4 &w, int i, F f) {
     w = make_uint4(ws[0], ws[1], ws[2], ws[3]);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte row accesses; kNT selects the non-temporal (streaming) cache policy
+template <bool kNT>
+__device__ inline uint4 ld16(const uint16_t *p) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+    const u32x4 v = kNT ? __builtin_nontemporal_load(q) : *q;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool kNT>
+__device__ inline void st16(uint16_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    u32x4 v;
+    v.x = a; v.y = b; v.z = c; v.w = d;
+    u32x4 *q = reinterpret_cast<u32x4 *>(p);
+    if (kNT) __builtin_nontemporal_store(v, q);
+    else *q = v;
+}
+
 __device__ inline uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
 
-template <bool kInit>
+// kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads
+template <bool kInit, int kPolicy>
 __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
+    constexpr bool kNtOwn = (kPolicy & 1) != 0, kNtSrc = (kPolicy & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // stride / 32 words
     __shared__ int32_t s_src[kMaxSegment];
     __shared__ int32_t s_raw[kMaxSegment];
@@ -129,15 +149,14 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             }
             e = make_uint4(ws[0], ws[1], ws[2], ws[3]);
         } else {
-            e = *reinterpret_cast<const uint4 *>(own_prev + col0);
+            e = ld16<kNtOwn>(own_prev + col0);
             e0 = e;
             for (int32_t j0 = 0; j0 < k; j0 += 4) {
                 uint4 v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (j0 + u < k)
-                        v[u] = *reinterpret_cast<const uint4 *>(
-                            a.prev + int64_t(s_src[j0 + u] - a.row0) * stride + col0);
+                        v[u] = ld16<kNtSrc>(a.prev + int64_t(s_src[j0 + u] - a.row0) * stride + col0);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (j0 + u >= k) break;
@@ -178,7 +197,7 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             bits |= (ent ? 1u : 0u) << i;
         }
         live += __builtin_popcount(bits);
-        *reinterpret_cast<uint4 *>(own_cur + col0) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
+        st16<kNtOwn>(own_cur + col0, ws[0], ws[1], ws[2], ws[3]);
         // presence bitmap: 8 bits per lane -> byte (col0 / 8)
         reinterpret_cast<uint8_t *>(s_bits)[col0 >> 3] = uint8_t(bits);
     }
@@ -270,22 +289,19 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     }
 }
 
-__global__ void __launch_bounds__(1024) exclusive_scan_kernel(const int32_t *deg, int32_t *off,
-                                                             int32_t n) {
-    __shared__ int32_t s_wave[16];
-    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int32_t per = (n + 1023) / 1024;
-    const int32_t b = tid * per;
-    int32_t local = 0;
-    for (int32_t i = 0; i < per; ++i)
-        if (b + i < n) local += deg[b + i];
-    int32_t incl = local;
+// Exclusive scan of the destination counts, two launches: (1) every 1024-thread block sums
+// its kScanTile elements; (2) every block adds the sums of the blocks before it (at most
+// a few hundred values, read from L2) to an in-block scan of its tile.
+constexpr int kScanThreads = 1024, kScanPer = 4, kScanTile = kScanThreads * kScanPer;
+
+__device__ inline int32_t block_scan_incl(int32_t v, int32_t *s_wave) {
+    const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const int32_t u = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += u;
+        const int32_t u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
     }
-    if (lane == 63) s_wave[wave] = incl;
+    if (lane == 63) s_wave[wave] = v;
     __syncthreads();
     if (wave == 0) {
         int32_t w = lane < 16 ? s_wave[lane] : 0;
@@ -297,14 +313,49 @@ __global__ void __launch_bounds__(1024) exclusive_scan_kernel(const int32_t *deg
         if (lane < 16) s_wave[lane] = w;
     }
     __syncthreads();
-    int32_t run = incl - local + (wave ? s_wave[wave - 1] : 0);
-    for (int32_t i = 0; i < per; ++i) {
-        if (b + i < n) {
-            off[b + i] = run;
-            run += deg[b + i];
-        }
+    return v + (wave ? s_wave[wave - 1] : 0);
+}
+
+__global__ void __launch_bounds__(kScanThreads) tile_sum_kernel(const int32_t *deg, int32_t n,
+                                                                int32_t *tile_sum) {
+    __shared__ int32_t s_wave[16];
+    const int64_t base = int64_t(blockIdx.x) * kScanTile + int64_t(threadIdx.x) * kScanPer;
+    int32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i)
+        if (base + i < n) v += deg[base + i];
+    const int32_t incl = block_scan_incl(v, s_wave);
+    if (threadIdx.x == kScanThreads - 1) tile_sum[blockIdx.x] = incl;
+}
+
+__global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(const int32_t *deg, int32_t n,
+                                                                 const int32_t *tile_sum,
+                                                                 int32_t *off) {
+    __shared__ int32_t s_wave[16];
+    __shared__ int32_t s_base;
+    if (threadIdx.x < 64) {
+        int32_t acc = 0;
+        for (int32_t b = threadIdx.x; b < int32_t(blockIdx.x); b += 64) acc += tile_sum[b];
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+        if (threadIdx.x == 0) s_base = acc;
     }
-    if (tid == 1023) off[n] = s_wave[15];
+    __syncthreads();
+    const int64_t base = int64_t(blockIdx.x) * kScanTile + int64_t(threadIdx.x) * kScanPer;
+    int32_t v[kScanPer];
+    int32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        v[i] = base + i < n ? deg[base + i] : 0;
+        sum += v[i];
+    }
+    int32_t run = block_scan_incl(sum, s_wave) - sum + s_base;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        if (base + i < n) off[base + i] = run;
+        run += v[i];
+    }
+    if (base < n && base + kScanPer >= n) off[n] = run;   // the thread holding element n-1
 }
 
 __global__ void scatter_kernel(const int32_t *out_dst, int64_t slots, int32_t fanout,
@@ -325,20 +376,29 @@ size_t scale_lds_bytes(int64_t stride) { return size_t(stride / 8); }
 
 hipError_t launch_scale_init(const ScaleTickArgs &a, hipStream_t st) {
     if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(scale_tick_kernel<true>, dim3(a.rows), dim3(kScaleBlock),
+    hipLaunchKernelGGL((scale_tick_kernel<true, 0>), dim3(a.rows), dim3(kScaleBlock),
                        scale_lds_bytes(a.stride), st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scale_tick(const ScaleTickArgs &a, hipStream_t st) {
+hipError_t launch_scale_tick(const ScaleTickArgs &a, int policy, hipStream_t st) {
     if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(scale_tick_kernel<false>, dim3(a.rows), dim3(kScaleBlock),
-                       scale_lds_bytes(a.stride), st, a);
+    const size_t lds = scale_lds_bytes(a.stride);
+    switch (policy & 3) {
+        case 0: hipLaunchKernelGGL((scale_tick_kernel<false, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
+        case 1: hipLaunchKernelGGL((scale_tick_kernel<false, 1>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
+        case 2: hipLaunchKernelGGL((scale_tick_kernel<false, 2>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
+        default: hipLaunchKernelGGL((scale_tick_kernel<false, 3>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, hipStream_t st) {
-    hipLaunchKernelGGL(exclusive_scan_kernel, dim3(1), dim3(1024), 0, st, deg, off, n);
+hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, int32_t *tile_sum,
+                                 hipStream_t st) {
+    const int32_t tiles = (n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(tile_sum_kernel, dim3(tiles), dim3(kScanThreads), 0, st, deg, n, tile_sum);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(tiles), dim3(kScanThreads), 0, st, deg, n, tile_sum,
+                       off);
     return hipGetLastError();
 }
 

@@ -49,9 +49,11 @@ struct ScaleTickArgs {
 };
 
 hipError_t launch_scale_init(const ScaleTickArgs &a, hipStream_t st);
-hipError_t launch_scale_tick(const ScaleTickArgs &a, hipStream_t st);
-// off[0..n] = exclusive scan of deg[0..n)
-hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, hipStream_t st);
+// policy: cache policy of the row streams (bit 0 own row non-temporal, bit 1 sender rows)
+hipError_t launch_scale_tick(const ScaleTickArgs &a, int policy, hipStream_t st);
+// off[0..n] = exclusive scan of deg[0..n); tile_sum holds ceil(n / 4096) ints of scratch
+hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, int32_t *tile_sum,
+                                 hipStream_t st);
 // csr_src[off[d] + k] = sender, for every message slot i with out_dst[i] = d >= 0
 hipError_t launch_scatter(const int32_t *out_dst, int64_t slots, int32_t fanout, int32_t row0,
                           const int32_t *off, int32_t *fill, int32_t *csr_src, hipStream_t st);

@@ -85,6 +85,9 @@ class ScaleEngine:
     def set_timing(self, on):
         check(lib().gsp_scale_set_timing(self._h, int(on)), "gsp_scale_set_timing")
 
+    def set_cache_policy(self, policy):
+        check(lib().gsp_scale_set_cache_policy(self._h, int(policy)), "gsp_scale_set_cache_policy")
+
     def stream(self):
         s = ctypes.c_void_p()
         check(lib().gsp_scale_hip_stream(self._h, ctypes.byref(s)), "gsp_scale_hip_stream")

@@ -227,6 +227,10 @@ int gsp_scale_messages(gsp_scale *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out);
 /* Enable/disable per-launch HIP event timing (default on). */
 int gsp_scale_set_timing(gsp_scale *s, int32_t on);
+/* Cache policy of the row streams of the fused tick kernel: bit 0 = non-temporal loads
+ * and stores of the receiver's own row, bit 1 = non-temporal loads of sender rows.
+ * Results are identical for every policy; only speed differs. */
+int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy);
 /* The hipStream_t (as void*) every launch of this engine is ordered on, so a caller can
  * bracket a timed region with its own HIP events on the same stream. */
 int gsp_scale_hip_stream(gsp_scale *s, void **stream);

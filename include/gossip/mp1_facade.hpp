@@ -1,0 +1,441 @@
+// include/gossip/mp1_facade.hpp -- the reference's MP1 class surface over the C ABI.
+//
+// A driver written against the reference headers (/root/reference/{Member,Params,Log,
+// EmulNet,MP1Node,Queue}.h) compiles against this header instead and runs on the MI355X
+// engine: same class names, same public fields, same method names and signatures, same
+// return conventions.  The classes are thin: every MP1Node / EmulNet call is RECORDED and
+// the calls of one phase are flushed to the engine as one batch (gsp_tick_recv /
+// gsp_tick_process), where the HIP kernels run them for all recorded nodes at once.  A
+// flush happens whenever the observable order requires it: a Log::LOG line from the
+// driver, a change of tick / phase / Params::dropmsg, a node recorded twice in one phase,
+// EmulNet::ENsend/ENcleanup, or MP1Node::syncMember().
+//
+// Member is a host mirror.  bFailed and addr are driver-owned (Application::fail writes
+// bFailed directly, Application.cpp:186/194); inited / inGroup / heartbeat are refreshed
+// after every batch; memberList is refreshed by MP1Node::syncMember() (one device read).
+//
+// Differences the batched engine imposes (documented in INTEGRATION.md):
+//   * recvCallBack(env, data, size) is executed inside checkMessages batches; a direct
+//     call with a raw buffer is rejected (returns false) because queued messages live in
+//     the engine, not in host memory;
+//   * ENrecv's enqueue callback and queue arguments are ignored for the same reason.
+#pragma once
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include "gossip/gossip.h"
+
+#ifndef SUCCESS
+#define SUCCESS 0
+#endif
+#ifndef FAILURE
+#define FAILURE -1
+#endif
+
+#define TREMOVE 20
+#define TFAIL 5
+
+class q_elt {
+public:
+    void *elt;
+    int size;
+    q_elt(void *e, int s) : elt(e), size(s) {}
+};
+
+class Address {
+public:
+    char addr[6];
+    Address() { std::memset(addr, 0, sizeof addr); }
+    Address(const Address &o) { std::memcpy(addr, o.addr, sizeof addr); }
+    explicit Address(const std::string &a) {
+        const size_t c = a.find(':');
+        const int id = std::stoi(a.substr(0, c));
+        const short port = short(std::stoi(a.substr(c + 1)));
+        std::memcpy(&addr[0], &id, 4);
+        std::memcpy(&addr[4], &port, 2);
+    }
+    Address &operator=(const Address &o) {
+        std::memcpy(addr, o.addr, sizeof addr);
+        return *this;
+    }
+    bool operator==(const Address &o) const { return std::memcmp(addr, o.addr, sizeof addr) == 0; }
+    int id() const { int v; std::memcpy(&v, &addr[0], 4); return v; }
+    short port() const { short v; std::memcpy(&v, &addr[4], 2); return v; }
+    std::string getAddress() { return std::to_string(id()) + ":" + std::to_string(port()); }
+    void init() { std::memset(addr, 0, sizeof addr); }
+};
+
+class MemberListEntry {
+public:
+    int id = 0;
+    short port = 0;
+    long heartbeat = 0;
+    long timestamp = 0;
+    MemberListEntry() = default;
+    MemberListEntry(int i, short p, long h, long t) : id(i), port(p), heartbeat(h), timestamp(t) {}
+    MemberListEntry(int i, short p) : id(i), port(p) {}
+    int getid() { return id; }
+    short getport() { return port; }
+    long getheartbeat() { return heartbeat; }
+    long gettimestamp() { return timestamp; }
+    void setid(int v) { id = v; }
+    void setport(short v) { port = v; }
+    void setheartbeat(long v) { heartbeat = v; }
+    void settimestamp(long v) { timestamp = v; }
+};
+
+class Member {
+public:
+    Address addr;
+    bool inited = false;
+    bool inGroup = false;
+    bool bFailed = false;
+    int nnb = 0;
+    long heartbeat = 0;
+    int pingCounter = 0;
+    int timeOutCounter = 0;
+    std::vector<MemberListEntry> memberList;
+    std::vector<MemberListEntry>::iterator myPos;
+    std::queue<q_elt> mp1q;   // kept for source compatibility; queues live in the engine
+    virtual ~Member() {}
+};
+
+class Params {
+public:
+    int MAX_NNB = 0;
+    int SINGLE_FAILURE = 0;
+    double MSG_DROP_PROB = 0;
+    double STEP_RATE = 0.25;
+    int EN_GPSZ = 0;
+    int MAX_MSG_SIZE = 4000;
+    int DROP_MSG = 0;
+    int dropmsg = 0;
+    int globaltime = 0;
+    int allNodesJoined = 0;
+    short PORTNUM = 8001;
+    gsp_params raw{};
+
+    Params() { gsp_params_default(&raw); }
+    void setparams(char *config_file) {
+        if (gsp_params_from_conf(config_file, &raw) != GSP_OK) {
+            std::fprintf(stderr, "%s\n", gsp_last_error());
+            std::exit(1);
+        }
+        MAX_NNB = raw.max_nnb;
+        SINGLE_FAILURE = raw.single_failure;
+        DROP_MSG = raw.drop_msg;
+        MSG_DROP_PROB = raw.msg_drop_prob;
+        EN_GPSZ = MAX_NNB;
+        STEP_RATE = raw.step_rate;
+        MAX_MSG_SIZE = raw.max_msg_size;
+        globaltime = 0;
+        dropmsg = 0;
+        allNodesJoined = 0;
+        for (int i = 0; i < EN_GPSZ; ++i) allNodesJoined += i;
+    }
+    int getcurrtime() { return globaltime; }
+};
+
+namespace gsp_facade {
+
+// Process-wide state shared by the facade objects (the reference's classes share state
+// through static / global variables as well: Log.cpp:46-54, Application.h nodeCount).
+struct Context {
+    gsp_engine *engine = nullptr;
+    Params *par = nullptr;
+    std::vector<Member *> members;          // by node index (id - 1)
+    int kind = 0;                           // 0 none, 1 recv batch, 2 process batch
+    int tick = -1, dropmsg = 0;
+    std::vector<int32_t> order;
+    std::vector<int8_t> ops;
+    std::vector<char> in_batch;
+
+    static void die(const char *what) {
+        std::fprintf(stderr, "gossip engine: %s failed: %s\n", what, gsp_last_error());
+        std::exit(1);
+    }
+    void require_engine() {
+        if (!engine) {
+            std::fprintf(stderr, "gossip engine: no EmulNet was constructed\n");
+            std::exit(1);
+        }
+    }
+
+    void flush() {
+        if (kind == 1) {
+            if (gsp_tick_recv(engine, tick, order.data(), int32_t(order.size())) != GSP_OK)
+                die("gsp_tick_recv");
+        } else if (kind == 2) {
+            if (gsp_tick_process(engine, tick, order.data(), ops.data(), int32_t(order.size()),
+                                 dropmsg) != GSP_OK)
+                die("gsp_tick_process");
+            for (int32_t node : order) refresh(node);
+        }
+        for (int32_t node : order) in_batch[size_t(node)] = 0;
+        order.clear();
+        ops.clear();
+        kind = 0;
+    }
+
+    void refresh(int32_t node) {
+        gsp_member_view v;
+        if (gsp_get_member(engine, node, &v) != GSP_OK) die("gsp_get_member");
+        Member *m = members[size_t(node)];
+        if (!m) return;
+        m->inited = v.inited != 0;
+        m->inGroup = v.in_group != 0;
+        m->heartbeat = long(v.heartbeat);
+        m->nnb = v.n_members;
+    }
+
+    void record(int k, int32_t node, int8_t op) {
+        require_engine();
+        const int t = par->getcurrtime();
+        const int dm = par->dropmsg;
+        if (kind != 0 && (kind != k || tick != t || (k == 2 && dropmsg != dm) ||
+                          in_batch[size_t(node)]))
+            flush();
+        kind = k;
+        tick = t;
+        dropmsg = dm;
+        order.push_back(node);
+        ops.push_back(op);
+        in_batch[size_t(node)] = 1;
+    }
+};
+
+inline Context &ctx() {
+    static Context c;
+    return c;
+}
+
+inline int32_t node_of(const Address *a) { return a ? a->id() - 1 : -1; }
+
+}  // namespace gsp_facade
+
+class Log {
+public:
+    explicit Log(Params *p) : par(p) {
+        // the reference opens dbg.log and an (unused) stats.log on the first LOG call
+        // (Log.cpp:56-69); the engine owns dbg.log, stats.log is created empty here
+        if (FILE *f = std::fopen("stats.log", "w")) std::fclose(f);
+    }
+    virtual ~Log() {}
+    void LOG(Address *addr, const char *str, ...) {
+        char text[30000];
+        va_list ap;
+        va_start(ap, str);
+        std::vsnprintf(text, sizeof text, str, ap);
+        va_end(ap);
+        auto &c = gsp_facade::ctx();
+        c.require_engine();
+        c.flush();
+        if (gsp_log(c.engine, gsp_facade::node_of(addr), par->getcurrtime(), text) != GSP_OK)
+            c.die("gsp_log");
+    }
+    void logNodeAdd(Address *self, Address *added) { member_line(self, added, "joined"); }
+    void logNodeRemove(Address *self, Address *removed) { member_line(self, removed, "removed"); }
+
+private:
+    void member_line(Address *self, Address *who, const char *verb) {
+        char line[128];
+        std::snprintf(line, sizeof line, "Node %d.%d.%d.%d:%d %s at time %d", who->addr[0],
+                      who->addr[1], who->addr[2], who->addr[3], int(who->port()), verb,
+                      par->getcurrtime());
+        LOG(self, "%s", line);
+    }
+    Params *par;
+};
+
+class EmulNet {
+public:
+    // The engine is created here (the reference's EmulNet owns the network state).  The
+    // reference seeds rand() with srand(time(NULL)) (Application.cpp:50/96); the facade uses
+    // the same seed -- time(NULL) -- unless GSP_SEED is set; GSP_RNG=philox selects the
+    // counter-based replay stream; GSP_DEVICE selects the HIP device.
+    explicit EmulNet(Params *p) : par(p) {
+        auto &c = gsp_facade::ctx();
+        const char *s = std::getenv("GSP_SEED");
+        const uint64_t seed = s && *s ? std::strtoull(s, nullptr, 10) : uint64_t(std::time(nullptr));
+        const char *m = std::getenv("GSP_RNG");
+        const gsp_rng_mode rng = (m && std::strcmp(m, "philox") == 0) ? GSP_RNG_PHILOX : GSP_RNG_GLIBC;
+        const char *d = std::getenv("GSP_DEVICE");
+        const int dev = d && *d ? std::atoi(d) : 0;
+        if (gsp_create(&p->raw, dev, rng, seed, "dbg.log", &c.engine) != GSP_OK)
+            c.die("gsp_create");
+        c.par = p;
+        c.members.assign(size_t(p->EN_GPSZ), nullptr);
+        c.in_batch.assign(size_t(p->EN_GPSZ), 0);
+    }
+    virtual ~EmulNet() {
+        auto &c = gsp_facade::ctx();
+        if (c.engine) {
+            c.flush();
+            gsp_destroy(c.engine);
+            c.engine = nullptr;
+        }
+    }
+    void *ENinit(Address *myaddr, short /*port*/) {   // ids 1, 2, ... (EmulNet.cpp:72-77)
+        const int id = nextid++;
+        const short port = 0;
+        std::memcpy(&myaddr->addr[0], &id, 4);
+        std::memcpy(&myaddr->addr[4], &port, 2);
+        return myaddr;
+    }
+    int ENsend(Address *myaddr, Address *toaddr, char *data, int size);
+    int ENsend(Address *myaddr, Address *toaddr, std::string data) {
+        return ENsend(myaddr, toaddr, const_cast<char *>(data.data()), int(data.size()));
+    }
+    // The next rand() of the engine's global draw order.  The reference's Application::fail
+    // calls libc rand() (Application.cpp:182/189), which shares its stream with the draws of
+    // ENsend (EmulNet.cpp:89); with the draws inside the engine, fail() calls this instead.
+    int ENrand() {
+        auto &c = gsp_facade::ctx();
+        c.require_engine();
+        c.flush();
+        int32_t v = 0;
+        if (gsp_rand(c.engine, par->getcurrtime(), &v) != GSP_OK) c.die("gsp_rand");
+        return v;
+    }
+    int ENrecv(Address *myaddr, int (*)(void *, char *, int), struct timeval *, int, void *) {
+        gsp_facade::ctx().record(1, gsp_facade::node_of(myaddr), 0);
+        return 0;
+    }
+    int ENcleanup() {   // writes msgcount.log for ticks [0, globaltime) (EmulNet.cpp:184-220)
+        auto &c = gsp_facade::ctx();
+        c.require_engine();
+        c.flush();
+        if (gsp_write_msgcount(c.engine, "msgcount.log", par->getcurrtime()) != GSP_OK)
+            c.die("gsp_write_msgcount");
+        gsp_flush_log(c.engine);
+        return 0;
+    }
+
+private:
+    Params *par;
+    int nextid = 1;
+};
+
+enum MsgTypes { JOINREQ, JOINREP, DUMMYLASTMSGTYPE, GOSSIP };
+
+typedef struct MessageHdr {
+    enum MsgTypes msgType;
+    Address *addr;
+    std::vector<MemberListEntry> vector_list;
+} MessageHdr;
+
+inline int EmulNet::ENsend(Address *myaddr, Address *toaddr, char *data, int /*size*/) {
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    c.flush();
+    const MessageHdr *h = reinterpret_cast<const MessageHdr *>(data);
+    int32_t admitted = 0;
+    if (gsp_send(c.engine, par->getcurrtime(), gsp_facade::node_of(myaddr), toaddr->id(),
+                 int32_t(h->msgType), par->dropmsg, &admitted) != GSP_OK)
+        c.die("gsp_send");
+    return admitted;
+}
+
+class Queue {
+public:
+    static bool enqueue(std::queue<q_elt> *q, void *buffer, int size) {
+        q->emplace(buffer, size);
+        return true;
+    }
+};
+
+class MP1Node {
+public:
+    MP1Node(Member *member, Params *params, EmulNet *emul, Log *log, Address *address)
+        : memberNode(member), par(params), emulNet(emul), log(log) {
+        memberNode->addr = *address;
+        auto &c = gsp_facade::ctx();
+        const int32_t node = gsp_facade::node_of(address);
+        if (node >= 0 && size_t(node) < c.members.size()) c.members[size_t(node)] = member;
+    }
+    virtual ~MP1Node() {}
+    Member *getMemberNode() { return memberNode; }
+
+    int recvLoop() {
+        if (memberNode->bFailed) return false;
+        return emulNet->ENrecv(&memberNode->addr, enqueueWrapper, nullptr, 1, &memberNode->mp1q);
+    }
+    static int enqueueWrapper(void *env, char *buff, int size) {
+        return Queue::enqueue(static_cast<std::queue<q_elt> *>(env), buff, size);
+    }
+    void nodeStart(char * /*servaddrstr*/, short /*serverport*/) {
+        // initThisNode + introduceSelfToGroup (MP1Node.cpp:95-154); the mirror is reset now,
+        // the engine runs the start in the next process batch
+        memberNode->bFailed = false;
+        memberNode->inited = true;
+        memberNode->inGroup = false;
+        memberNode->nnb = 0;
+        memberNode->heartbeat = 0;
+        memberNode->pingCounter = TFAIL;
+        memberNode->timeOutCounter = -1;
+        memberNode->memberList.clear();
+        gsp_facade::ctx().record(2, node(), GSP_OP_START);
+    }
+    int initThisNode(Address *) { return 0; }
+    int introduceSelfToGroup(Address *) { return 1; }
+    int finishUpThisNode() {
+        gsp_facade::ctx().flush();
+        memberNode->inited = false;
+        memberNode->inGroup = false;
+        memberNode->heartbeat = 0;
+        memberNode->memberList.clear();
+        return 0;
+    }
+    void nodeLoop() {
+        if (memberNode->bFailed) return;
+        gsp_facade::ctx().record(2, node(), GSP_OP_LOOP);
+    }
+    void checkMessages() { gsp_facade::ctx().record(2, node(), GSP_OP_CHECK); }
+    bool recvCallBack(void *, char *, int) { return false; }
+    void nodeLoopOps() { gsp_facade::ctx().record(2, node(), GSP_OP_OPS); }
+    int isNullAddress(Address *a) {
+        static const char zero[6] = {0};
+        return std::memcmp(a->addr, zero, 6) == 0 ? 1 : 0;
+    }
+    Address getJoinAddress() {
+        Address a;
+        const int id = 1;
+        std::memcpy(&a.addr[0], &id, 4);
+        return a;
+    }
+    void initMemberListTable(Member *m) { m->memberList.clear(); }
+    void printAddress(Address *a) {
+        std::printf("%d.%d.%d.%d:%d \n", a->addr[0], a->addr[1], a->addr[2], a->addr[3],
+                    int(a->port()));
+    }
+    // Flush pending work and copy this node's member list from the device into the mirror.
+    Member *syncMember() {
+        auto &c = gsp_facade::ctx();
+        c.flush();
+        c.refresh(node());
+        std::vector<gsp_entry> buf(size_t(par->EN_GPSZ) + 1);
+        int32_t n = 0;
+        if (gsp_member_list(c.engine, node(), buf.data(), int32_t(buf.size()), &n) != GSP_OK)
+            c.die("gsp_member_list");
+        memberNode->memberList.clear();
+        for (int32_t i = 0; i < n; ++i)
+            memberNode->memberList.emplace_back(buf[size_t(i)].id, buf[size_t(i)].port,
+                                                long(buf[size_t(i)].heartbeat),
+                                                long(buf[size_t(i)].timestamp));
+        return memberNode;
+    }
+
+private:
+    int32_t node() const { return gsp_facade::node_of(&memberNode->addr); }
+    Member *memberNode;
+    Params *par;
+    EmulNet *emulNet;
+    Log *log;
+};

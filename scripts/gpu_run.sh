@@ -1,15 +1,29 @@
 #!/bin/bash
+# One GPU session: tests, bench, policy A/B, rocprof kernel trace + PMC passes.
+# usage: bash scripts/gpu_run.sh <tag>
 cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
+TAG=${1:-r}
+OUT="$GRAFT_REPO_ROOT/gpurun_out/$TAG"
+mkdir -p "$OUT"
 export TMPDIR=/tmp
-nproc; rocm-smi --showproductname 2>/dev/null | head -5
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r1_tests.log 2>&1
-rc=$?
-echo "tests rc=$rc"
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 240 python -u bench.py > gpurun_out/r1_bench.json 2> gpurun_out/r1_bench.err
-rc=$?
-echo "bench rc=$rc"; cat gpurun_out/r1_bench.json
-if [ $rc -ne 0 ]; then exit $rc; fi
-cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof1" -o bench --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/r1_prof.log" 2>&1
-echo "prof rc=$?"
+step() {   # step <name> <timeout> cmd...; stop the session on a crash / timeout
+    local name=$1 to=$2; shift 2
+    timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+    return 0
+}
+step tests 420 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
+step bench 240 python -u bench.py
+cat "$OUT/bench.log" | tail -1
+step ab 200 python -u scripts/ab_policy.py 65536 4
+tail -1 "$OUT/ab.log"
+cd /tmp
+BENCH="$GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 5 --no-cpu-baseline"
+step prof_trace 200 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 $BENCH
+step pmc_fetch 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 $BENCH
+step pmc_write 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python3 $BENCH
+step pmc_sq 120 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmc_sq" -o run --output-format csv -- python3 $BENCH
+step pmc_tcc 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/pmc_tcc" -o run --output-format csv -- python3 $BENCH
+echo done

@@ -16,6 +16,7 @@ import re
 
 import pytest
 
+from tests import grader
 from tests.oracle_binding import (CONFS, FILES, GOLDEN, MODES, SEEDS, golden, load_oracle,
                                   run_oracle_mp1)
 
@@ -67,42 +68,11 @@ def test_oracle_philox_known_answers(ctr, key, want):
     assert tuple(o) == want
 
 
-def _grader(dbg, conf):
-    """Grader.sh's scoring of one dbg.log (Grader.sh:29-190), in Python."""
-    lines = dbg.decode().split("\n")
-    joined = [l for l in lines if "joined" in l]
-    removed = sorted(set(l for l in lines if "removed" in l))
-    fails = sorted(set(l for l in lines if "Node failed at time" in l))
-    pts = 0
-    # join: every node lists 9 distinct peers (Grader.sh:40-60)
-    peers = {}
-    for l in joined:
-        f = l.split(" ")
-        peers.setdefault(f[1], set()).add(" ".join(f[3:7]))
-    pts += 10 if len(peers) == 10 and all(len(v) == 9 for v in peers.values()) else 0
-    failed_nodes = [l.split()[0] for l in fails]
-    if conf in ("singlefailure", "msgdropsinglefailure"):
-        fn = failed_nodes[0]
-        fc = len([l for l in removed if fn in l])
-        pts += 10 if fc >= 9 else 0
-        if conf == "singlefailure":
-            acc = len([l for l in removed if fn not in l])
-            pts += 10 if acc == 0 and fc > 0 else 0
-        else:
-            pts += 10  # accuracy not graded for the drop case (Grader.sh:181-189)
-    else:
-        ok_c = all(len([l for l in removed if fn in l]) >= 5 for fn in failed_nodes)
-        pts += 10 if ok_c else 0
-        ok_a = all(len([l for l in removed if fn not in l]) == 20 for fn in failed_nodes)
-        pts += 10 if ok_a else 0
-    return pts
-
-
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("seed", SEEDS)
 def test_grader_checks_hold_on_golden(mode, seed):
     for conf in CONFS:
-        assert _grader(golden(mode, conf, seed, "dbg.log"), conf) == 30, (mode, conf, seed)
+        assert grader.score(golden(mode, conf, seed, "dbg.log"), conf) == 30, (mode, conf, seed)
 
 
 def test_golden_state_shape():
