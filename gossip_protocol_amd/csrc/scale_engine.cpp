@@ -26,7 +26,9 @@ struct gsp_scale {
     bool timing = true;
     gsp::DevBuf<uint16_t> table[2];
     gsp::DevBuf<int32_t> own_hb, fail_tick, cnt[2], out_dst, deg, off, fill, csr_src, err, tile_sum;
-    int policy = 0;   // cache policy of the row streams (scale_kernels.hpp)
+    // cache policy of the row streams (scale_kernels.hpp); 1 = non-temporal own row, the
+    // fastest in the A/B of profiles/r01/r2/ab_policy.json (7.52 vs 7.89 ms per launch)
+    int policy = 1;
     gsp::DevBuf<unsigned long long> dig;
     std::vector<int32_t> h_fail;
     struct Timed { hipEvent_t a, b, c; };
