@@ -9,8 +9,10 @@ peers (the reference's nodeLoop, /root/reference/MP1Node.cpp:176-362, at scale).
 
 N = 1: BASELINE config 3 -- 65,536 nodes, full view (65,536 x 65,536 packed u16 table),
        fanout 3, 1% random crash at t = 10, no drops; ticks 1..W warm up, W+1..W+K timed.
-N > 1: rows sharded over N GPUs (one process per GPU, torch.distributed over RCCL for the
-       barrier / timing reduction), see DESIGN.md "Multi-GPU".
+N > 1: the same workload (strong scaling), column-sharded over N GPUs, one process per GPU;
+       the engine exchanges per-row counts and peer choices over its own RCCL communicator,
+       torch.distributed only carries the RCCL id, the barrier and the timing reductions
+       (DESIGN.md "Multi-GPU").
 Prints ONE JSON line (rank 0) with the roofline of the fused tick kernel and the CPU
 baseline (the oracle restatement, timed on a bounded sample of the same workload).
 """
@@ -83,10 +85,11 @@ def main():
     from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
 
     if world > 1:
-        from gossip_protocol_amd.shard import ShardedScaleEngine
-        eng = ShardedScaleEngine(args.nodes, fanout=FANOUT, fail_mode=FAIL_RANDOM,
-                                 fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM, seed=SEED,
-                                 max_ticks=args.warmup + args.steps, device=local)
+        # column shards: the same config-3 workload split N ways (strong scaling)
+        from gossip_protocol_amd.dist import make_rank_engine
+        eng = make_rank_engine(args.nodes, local, fanout=FANOUT, fail_mode=FAIL_RANDOM,
+                               fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM, seed=SEED,
+                               max_ticks=args.warmup + args.steps)
     else:
         eng = ScaleEngine(args.nodes, fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK,
                           fail_ppm=FAIL_PPM, seed=SEED, max_ticks=args.warmup + args.steps,
@@ -115,15 +118,27 @@ def main():
         rounds += d["node_rounds"]
         merges += d["merges"]
         delivered += d["delivered"]
-    stride = -(-args.nodes // 2048) * 2048
+    if dist is not None:
+        # every rank streams its slice of every processed row and of every sender row
+        tot = torch.tensor([rounds, delivered], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        rows_all, delivered_all = tot[0].item(), tot[1].item()
+    else:
+        rows_all, delivered_all = rounds, delivered
+    stride = eng.layout()[2]
     launches = perf1["merge_launches"] - perf0["merge_launches"]
     kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / max(launches, 1)
     csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / max(launches, 1)
     # algorithmic bytes per launch: own row read + write, one sender row per message
     # (2-byte entries), one 4-byte CSR entry per message
-    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) / args.steps
+    # per shard: its slice (stride columns) of every processed and every sender row; the
+    # job moves `world` slices (row counts are kept by rank 0 only, so rows_all = job total)
+    bytes_per_launch = ((2.0 * rows_all + delivered_all) * stride * 2.0 +
+                        delivered_all * 4.0) * world / args.steps
 
     if dist is not None:
+        # per-row counts live on rank 0 only (sum = job total); each rank moves its own
+        # slice's bytes (sum); the step time and kernel time are the slowest rank's (max)
         t = torch.tensor([el, rounds, merges, bytes_per_launch, kern_ms], dtype=torch.float64,
                          device="cuda")
         tmax = t.clone()
@@ -135,7 +150,8 @@ def main():
         kern_ms = tmax[4].item()
 
     if rank == 0:
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9     # summed over ranks
+        peak = PEAK_HBM_GBS * world
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(prof):
@@ -152,17 +168,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": el * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "weak" if world > 1 else "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u16",
             "data": "synthetic (pre-joined full-view membership, Philox peers/failures)",
             "config": {"workload": "config3: %d nodes full view, fanout %d, 1%% random crash at "
                                    "t=%d, no drops" % (args.nodes, FANOUT, FAIL_TICK),
                        "nodes": args.nodes, "view": args.nodes, "fanout": FANOUT,
-                       "entry_bytes": 2, "parallelism": "rows%d" % world},
+                       "entry_bytes": 2,
+                       "parallelism": "columns%d" % world if world > 1 else "1gpu"},
             "merges_per_s": merges / el,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak,
+                         "unit": "GB/s", "frac": achieved / peak, "traffic": traffic,
                          "kernel": "scale_tick_kernel", "kernel_ms": kern_ms,
                          "csr_ms": csr_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
         }

@@ -100,6 +100,13 @@ SIGNATURES = {
     "gsp_scale_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
     "gsp_scale_set_timing": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
     "gsp_scale_set_cache_policy": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_scale_set_merge": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_scale_nccl_id": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "gsp_scale_create_rank": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32, c_int32,
+                                             ctypes.c_void_p, P(ctypes.c_void_p)]),
+    "gsp_scale_create_group": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
+                                              P(ctypes.c_void_p)]),
+    "gsp_scale_layout": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), P(c_int64)]),
     "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
 }
 

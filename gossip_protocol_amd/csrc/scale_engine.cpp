@@ -1,11 +1,18 @@
 // gossip_protocol_amd/csrc/scale_engine.cpp -- host side of the SCALE engine (C ABI).
 //
-// One tick = four stream-ordered launches, no host synchronisation:
+// One GPU (fused): one tick = four stream-ordered launches, no host synchronisation:
 //   exclusive_scan(deg) -> off   receiver CSR offsets from last tick's destination counts
 //   scatter(out_dst)   -> csr    sender ids per receiver (order fixed later by the kernel)
 //   memset(deg)                  re-armed for this tick's sends
 //   scale_tick_kernel            merge + ops + events + send, one workgroup per row
-// The membership table lives in HBM as two [rows][stride] uint16 buffers (tick parity).
+// Column shards (G > 1): shard g owns columns [g*W, (g+1)*W) of EVERY row, so the merge is
+// entirely local; the only exchange per tick is
+//   all-gather of the per-row member counts of every slice     (n * 4 B per shard)
+//   all-reduce MAX of the resolved peer choices                (n * fanout * 4 B)
+// over RCCL (one process per GPU) or, for a group of shards inside one process, device
+// copies on the group's stream (used to test the sharded path on one GPU).
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -16,20 +23,54 @@
 #include "philox.hpp"
 #include "scale_kernels.hpp"
 
+namespace {
+
+struct Shard {
+    int32_t g = 0;
+    int32_t col0 = 0;
+    gsp::DevBuf<uint16_t> table[2];
+    gsp::DevBuf<int32_t> own_hb, fail_tick, cnt_total[2], cnt_slice, cnt_all, out_dst, picks,
+        deg, off, fill, csr_src, err, tile_sum;
+    gsp::DevBuf<uint8_t> bitmap;
+    gsp::DevBuf<unsigned long long> dig;
+
+    void release() {
+        for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
+        for (auto *x : {&own_hb, &fail_tick, &cnt_slice, &cnt_all, &out_dst, &picks, &deg, &off,
+                        &fill, &csr_src, &err, &tile_sum})
+            x->release();
+        bitmap.release();
+        dig.release();
+    }
+};
+
+#define GSP_NCCL(call)                                                                  \
+    do {                                                                                \
+        ncclResult_t gsp_r_ = (call);                                                   \
+        if (gsp_r_ != ncclSuccess) {                                                    \
+            ::gsp::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,         \
+                             ncclGetErrorString(gsp_r_));                               \
+            return GSP_ERR_RCCL;                                                        \
+        }                                                                               \
+    } while (0)
+
+}  // namespace
+
 struct gsp_scale {
     gsp_scale_params p{};
     int device = 0;
     hipStream_t st = nullptr;
-    int64_t stride = 0;
-    int32_t rows = 0, row0 = 0;
+    int32_t shards = 1;        // G: column shards in the whole job
+    int32_t rank = 0;          // first shard index held by this engine
+    bool sliced = false;       // column mode (G > 1)
+    ncclComm_t comm = nullptr; // one shard per process when set
+    int64_t width = 0;         // n rounded up to 2048 * G
+    int64_t stride = 0;        // columns per shard
     int32_t tick = 0;
     bool timing = true;
-    gsp::DevBuf<uint16_t> table[2];
-    gsp::DevBuf<int32_t> own_hb, fail_tick, cnt[2], out_dst, deg, off, fill, csr_src, err, tile_sum;
-    // cache policy of the row streams (scale_kernels.hpp); 1 = non-temporal own row, the
-    // fastest in the A/B of profiles/r01/r2/ab_policy.json (7.52 vs 7.89 ms per launch)
-    int policy = 1;
-    gsp::DevBuf<unsigned long long> dig;
+    int policy = 1;            // bit 0 nt own row, bit 1 nt sender rows (A/B: profiles/r01)
+    int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
+    std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
     std::vector<int32_t> h_fail;
     struct Timed { hipEvent_t a, b, c; };
     std::vector<Timed> pending;
@@ -47,31 +88,60 @@ struct gsp_scale {
         return e;
     }
 
-    gsp::ScaleTickArgs args(int32_t t) const {
+    gsp::ScaleTickArgs args(Shard &sh, int32_t t) const {
         gsp::ScaleTickArgs a{};
-        a.prev = table[(t + 1) & 1].p;
-        a.cur = table[t & 1].p;
+        a.prev = sh.table[(t + 1) & 1].p;
+        a.cur = sh.table[t & 1].p;
+        a.remote = nullptr;
         a.stride = stride;
         a.n = p.n;
-        a.row0 = row0;
-        a.rows = rows;
+        a.col0 = sh.col0;
+        a.row0 = 0;
+        a.rows = p.n;
         a.tick = t;
         a.tremove = p.tremove;
         a.fanout = p.fanout;
         a.drop_pct = p.drop_pct;
         a.h0 = p.h0;
+        a.nt_own = policy & 1;
+        a.nt_src = (policy >> 1) & 1;
+        a.count_rounds = sh.g == 0;
         a.seed = p.seed;
-        a.fail_tick = fail_tick.p;
-        a.own_hb = own_hb.p;
-        a.cnt_prev = cnt[(t + 1) & 1].p;
-        a.cnt_cur = cnt[t & 1].p;
-        a.off = off.p;
-        a.csr_src = csr_src.p;
-        a.out_dst = out_dst.p;
-        a.deg = deg.p;
-        a.dig = dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
-        a.err = err.p;
+        a.fail_tick = sh.fail_tick.p;
+        a.own_hb = sh.own_hb.p;
+        a.cnt_prev = sh.cnt_total[(t + 1) & 1].p;
+        a.cnt_cur = sliced ? sh.cnt_slice.p : sh.cnt_total[t & 1].p;
+        a.off = sh.off.p;
+        a.csr_src = sh.csr_src.p;
+        a.csr_slot = nullptr;
+        a.out_dst = sh.out_dst.p;
+        a.deg = sh.deg.p;
+        a.bitmap = sh.bitmap.p;
+        a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
+        a.err = sh.err.p;
         return a;
+    }
+
+    gsp::ScaleResolveArgs resolve_args(Shard &sh, int32_t t) const {
+        gsp::ScaleResolveArgs r{};
+        r.n = p.n;
+        r.fanout = p.fanout;
+        r.tick = t;
+        r.drop_pct = p.drop_pct;
+        r.shard = sh.g;
+        r.shards = shards;
+        r.count_rounds = sh.g == 0;
+        r.stride = stride;
+        r.seed = p.seed;
+        r.fail_tick = sh.fail_tick.p;
+        r.cnt_all = sh.cnt_all.p;
+        r.cnt_total = sh.cnt_total[t & 1].p;
+        r.bitmap = sh.bitmap.p;
+        r.picks = sh.picks.p;
+        r.out_dst = sh.out_dst.p;
+        r.deg = sh.deg.p;
+        r.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
+        return r;
     }
 };
 
@@ -114,40 +184,89 @@ int validate_scale_params(const gsp_scale_params *p) {
 
 namespace {
 
-int scale_alloc(gsp_scale *s) {
+int shard_alloc(gsp_scale *s, Shard &sh) {
     const int32_t n = s->p.n;
-    const size_t tab = size_t(s->rows) * size_t(s->stride);
+    const size_t tab = size_t(n) * size_t(s->stride);
+    hipStream_t st = s->st;
     for (int b = 0; b < 2; ++b) {
-        GSP_HIP(s->table[b].alloc(tab));
-        GSP_HIP(s->cnt[b].alloc(size_t(n)));
-        GSP_HIP(hipMemsetAsync(s->cnt[b].p, 0, size_t(n) * 4, s->st));
+        GSP_HIP(sh.table[b].alloc(tab));
+        GSP_HIP(sh.cnt_total[b].alloc(size_t(n)));
+        GSP_HIP(hipMemsetAsync(sh.cnt_total[b].p, 0, size_t(n) * 4, st));
     }
-    GSP_HIP(s->own_hb.alloc(size_t(s->rows)));
-    GSP_HIP(s->fail_tick.alloc(size_t(n)));
-    GSP_HIP(s->out_dst.alloc(size_t(s->rows) * s->p.fanout));
-    GSP_HIP(s->deg.alloc(size_t(n)));
-    GSP_HIP(s->off.alloc(size_t(n) + 1));
-    GSP_HIP(s->fill.alloc(size_t(n)));
-    GSP_HIP(s->csr_src.alloc(size_t(n) * s->p.fanout));
-    GSP_HIP(s->err.alloc(1));
-    GSP_HIP(s->tile_sum.alloc(size_t(n) / 4096 + 1));
+    GSP_HIP(sh.own_hb.alloc(size_t(n)));
+    GSP_HIP(sh.fail_tick.alloc(size_t(n)));
+    GSP_HIP(sh.out_dst.alloc(size_t(n) * s->p.fanout));
+    GSP_HIP(sh.deg.alloc(size_t(n)));
+    GSP_HIP(sh.off.alloc(size_t(n) + 1));
+    GSP_HIP(sh.fill.alloc(size_t(n)));
+    GSP_HIP(sh.csr_src.alloc(size_t(n) * s->p.fanout));
+    GSP_HIP(sh.err.alloc(1));
+    GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
+    if (s->sliced) {
+        GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
+        GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards));
+        GSP_HIP(sh.picks.alloc(size_t(n) * s->p.fanout));
+        GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8)));
+    }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
-    GSP_HIP(s->dig.alloc(dig));
-    GSP_HIP(hipMemsetAsync(s->dig.p, 0, dig * sizeof(unsigned long long), s->st));
-    GSP_HIP(hipMemsetAsync(s->own_hb.p, 0, size_t(s->rows) * 4, s->st));
-    GSP_HIP(hipMemsetAsync(s->deg.p, 0, size_t(n) * 4, s->st));
-    GSP_HIP(hipMemsetAsync(s->err.p, 0, 4, s->st));
-    GSP_HIP(hipMemcpyAsync(s->fail_tick.p, s->h_fail.data(), size_t(n) * 4, hipMemcpyHostToDevice,
-                           s->st));
+    GSP_HIP(sh.dig.alloc(dig));
+    GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
+    GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, size_t(n) * 4, st));
+    GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, st));
+    GSP_HIP(hipMemsetAsync(sh.err.p, 0, 4, st));
+    GSP_HIP(hipMemcpyAsync(sh.fail_tick.p, s->h_fail.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
+    return GSP_OK;
+}
+
+// all-gather of every shard's per-row slice counts into every shard's cnt_all[G][n]
+int exchange_counts(gsp_scale *s) {
+    const size_t n = size_t(s->p.n);
+    if (s->comm) {
+        Shard &sh = s->local[0];
+        GSP_NCCL(ncclAllGather(sh.cnt_slice.p, sh.cnt_all.p, n, ncclInt32, s->comm, s->st));
+        return GSP_OK;
+    }
+    for (Shard &dst : s->local)
+        for (Shard &src : s->local)
+            GSP_HIP(hipMemcpyAsync(dst.cnt_all.p + size_t(src.g) * n, src.cnt_slice.p, n * 4,
+                                   hipMemcpyDeviceToDevice, s->st));
+    return GSP_OK;
+}
+
+// all-reduce MAX of the resolved picks (each pick is resolved by exactly one shard)
+int exchange_picks(gsp_scale *s) {
+    const size_t cnt = size_t(s->p.n) * s->p.fanout;
+    if (s->comm) {
+        Shard &sh = s->local[0];
+        GSP_NCCL(ncclAllReduce(sh.picks.p, sh.picks.p, cnt, ncclInt32, ncclMax, s->comm, s->st));
+        return GSP_OK;
+    }
+    Shard &root = s->local[0];
+    for (size_t i = 1; i < s->local.size(); ++i)
+        GSP_HIP(gsp::launch_max_into(root.picks.p, s->local[i].picks.p, int64_t(cnt), s->st));
+    for (size_t i = 1; i < s->local.size(); ++i)
+        GSP_HIP(hipMemcpyAsync(s->local[i].picks.p, root.picks.p, cnt * 4, hipMemcpyDeviceToDevice,
+                               s->st));
+    return GSP_OK;
+}
+
+// message generation for tick t (columns: after the slices are merged)
+int resolve_sends(gsp_scale *s, int32_t t) {
+    if (int rc = exchange_counts(s)) return rc;
+    for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(sh, t), s->st));
+    if (int rc = exchange_picks(s)) return rc;
+    for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_finalize(s->resolve_args(sh, t), s->st));
     return GSP_OK;
 }
 
 int check_err(gsp_scale *s) {
-    int32_t err = 0;
-    GSP_HIP(hipMemcpyAsync(&err, s->err.p, 4, hipMemcpyDeviceToHost, s->st));
-    GSP_HIP(hipStreamSynchronize(s->st));
-    GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY,
-                "a receiver got more than %d messages in one tick", gsp::kMaxSegment);
+    for (Shard &sh : s->local) {
+        int32_t err = 0;
+        GSP_HIP(hipMemcpyAsync(&err, sh.err.p, 4, hipMemcpyDeviceToHost, s->st));
+        GSP_HIP(hipStreamSynchronize(s->st));
+        GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY, "a receiver got more than %d messages in one tick",
+                    gsp::kMaxSegment);
+    }
     return GSP_OK;
 }
 
@@ -168,39 +287,81 @@ int collect_timing(gsp_scale *s) {
     return GSP_OK;
 }
 
+int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t rank,
+                int32_t local_shards, const void *nccl_id, gsp_scale **out) {
+    GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_scale: out is NULL");
+    *out = nullptr;
+    if (int rc = gsp::validate_scale_params(p)) return rc;
+    GSP_REQUIRE(shards >= 1 && shards <= 64 && rank >= 0 && rank + local_shards <= shards,
+                GSP_ERR_INVALID, "gsp_scale: shards=%d rank=%d", shards, rank);
+    int ndev = 0;
+    GSP_HIP(hipGetDeviceCount(&ndev));
+    GSP_REQUIRE(device >= 0 && device < ndev, GSP_ERR_HIP, "gsp_scale: device %d of %d", device, ndev);
+    GSP_HIP(hipSetDevice(device));
+    std::unique_ptr<gsp_scale> s(new gsp_scale);
+    s->p = *p;
+    s->device = device;
+    s->shards = shards;
+    s->rank = rank;
+    s->sliced = shards > 1;
+    const int64_t unit = int64_t(gsp::kChunk) * shards;
+    s->width = (int64_t(p->n) + unit - 1) / unit * unit;
+    s->stride = s->width / shards;
+    s->h_fail = gsp::scale_fail_ticks(*p);
+    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 3;
+    if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
+    if (!s->sliced) {
+        // the fused kernel keeps the row's presence bitmap in LDS next to 8.3 KB of statics
+        GSP_REQUIRE(gsp::scale_lds_bytes(s->stride, false) <= 48 * 1024, GSP_ERR_CAPACITY,
+                    "row bitmap of %lld B exceeds the LDS budget (one-GPU full view n <= 393216)",
+                    (long long)(s->stride / 8));
+    }
+    GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    if (nccl_id) {
+        ncclUniqueId id;
+        std::memcpy(&id, nccl_id, sizeof id);
+        GSP_NCCL(ncclCommInitRank(&s->comm, shards, id, rank));
+    }
+    s->local.resize(size_t(local_shards));
+    for (int32_t i = 0; i < local_shards; ++i) {
+        Shard &sh = s->local[size_t(i)];
+        sh.g = rank + i;
+        sh.col0 = int32_t(int64_t(sh.g) * s->stride);
+        if (int rc = shard_alloc(s.get(), sh)) return rc;
+    }
+    for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_init(s->args(sh, 0), s->sliced, s->st));
+    if (s->sliced)
+        if (int rc = resolve_sends(s.get(), 0)) return rc;
+    GSP_HIP(hipStreamSynchronize(s->st));
+    *out = s.release();
+    return GSP_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
 int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out) {
-    GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_scale_create: out is NULL");
-    *out = nullptr;
-    if (int rc = gsp::validate_scale_params(p)) return rc;
-    int ndev = 0;
-    GSP_HIP(hipGetDeviceCount(&ndev));
-    GSP_REQUIRE(device >= 0 && device < ndev, GSP_ERR_HIP, "gsp_scale_create: device %d of %d",
-                device, ndev);
-    GSP_HIP(hipSetDevice(device));
-    std::unique_ptr<gsp_scale> s(new gsp_scale);
-    s->p = *p;
-    s->device = device;
-    s->stride = (int64_t(p->n) + gsp::kChunk - 1) / gsp::kChunk * gsp::kChunk;
-    s->rows = p->n;
-    s->row0 = 0;
-    s->h_fail = gsp::scale_fail_ticks(*p);
-    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 3;
-    GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
-    if (int rc = scale_alloc(s.get())) return rc;
-    const size_t lds = gsp::scale_lds_bytes(s->stride);
-    // the row's presence bitmap lives in LDS next to 8.3 KB of static scratch
-    GSP_REQUIRE(lds <= 48 * 1024, GSP_ERR_CAPACITY,
-                "row bitmap of %zu B exceeds the LDS budget (full view n <= 393216)", lds);
-    gsp::ScaleTickArgs a = s->args(0);
-    GSP_HIP(gsp::launch_scale_init(a, s->st));
-    GSP_HIP(hipStreamSynchronize(s->st));
-    s->tick = 0;
-    *out = s.release();
+    return scale_build(p, device, 1, 0, 1, nullptr, out);
+}
+
+int gsp_scale_create_group(const gsp_scale_params *p, int device, int32_t shards, gsp_scale **out) {
+    return scale_build(p, device, shards, 0, shards, nullptr, out);
+}
+
+int gsp_scale_nccl_id(void *out, size_t cap) {
+    GSP_REQUIRE(out && cap >= sizeof(ncclUniqueId), GSP_ERR_INVALID,
+                "gsp_scale_nccl_id: need %zu bytes", sizeof(ncclUniqueId));
+    ncclUniqueId id;
+    GSP_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof id);
     return GSP_OK;
+}
+
+int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
+                          const void *nccl_id, gsp_scale **out) {
+    GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_scale_create_rank: NULL nccl id");
+    return scale_build(p, device, world, rank, 1, world > 1 ? nccl_id : nullptr, out);
 }
 
 int gsp_scale_destroy(gsp_scale *s) {
@@ -213,11 +374,8 @@ int gsp_scale_destroy(gsp_scale *s) {
         s->free_events.push_back(t.c);
     }
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
-    for (int b = 0; b < 2; ++b) { s->table[b].release(); s->cnt[b].release(); }
-    for (auto *b : {&s->own_hb, &s->fail_tick, &s->out_dst, &s->deg, &s->off, &s->fill,
-                    &s->csr_src, &s->err, &s->tile_sum})
-        b->release();
-    s->dig.release();
+    for (Shard &sh : s->local) sh.release();
+    if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -229,7 +387,7 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
                 "gsp_scale_step: tick %d beyond max_ticks %d", s->tick + ticks, s->p.max_ticks);
     GSP_HIP(hipSetDevice(s->device));
     const int32_t n = s->p.n;
-    const int64_t slots = int64_t(s->rows) * s->p.fanout;
+    const int64_t slots = int64_t(n) * s->p.fanout;
     for (int32_t i = 0; i < ticks; ++i) {
         const int32_t t = s->tick + 1;
         gsp_scale::Timed tm{};
@@ -237,17 +395,22 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
             tm = {s->event(), s->event(), s->event()};
             GSP_HIP(hipEventRecord(tm.a, s->st));
         }
-        GSP_HIP(gsp::launch_exclusive_scan(s->deg.p, s->off.p, n, s->tile_sum.p, s->st));
-        GSP_HIP(hipMemsetAsync(s->fill.p, 0, size_t(n) * 4, s->st));
-        GSP_HIP(gsp::launch_scatter(s->out_dst.p, slots, s->p.fanout, s->row0, s->off.p, s->fill.p,
-                                    s->csr_src.p, s->st));
-        GSP_HIP(hipMemsetAsync(s->deg.p, 0, size_t(n) * 4, s->st));
+        for (Shard &sh : s->local) {
+            GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
+            GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
+            GSP_HIP(gsp::launch_scatter(sh.out_dst.p, slots, s->p.fanout, 0, sh.off.p, sh.fill.p,
+                                        sh.csr_src.p, s->st));
+            GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
+        }
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
-        GSP_HIP(gsp::launch_scale_tick(s->args(t), s->policy, s->st));
+        for (Shard &sh : s->local)
+            GSP_HIP(gsp::launch_scale_tick(s->args(sh, t), s->sliced, s->merge, s->st));
         if (s->timing) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);
         }
+        if (s->sliced)
+            if (int rc = resolve_sends(s, t)) return rc;
         s->tick = t;
         s->perf.ticks++;
     }
@@ -268,16 +431,21 @@ int gsp_scale_tick(gsp_scale *s, int32_t *tick) {
     return GSP_OK;
 }
 
+// Digest of this engine's shards.  Per-column quantities (joins, removes, hash) are summed
+// over the shards held here; per-row quantities are counted by shard 0 only.  In the
+// one-process-per-GPU case the job's digest is the sum of every rank's digest.
 int gsp_scale_digest_get(gsp_scale *s, int32_t t, gsp_scale_digest *out) {
     GSP_REQUIRE(s && out, GSP_ERR_INVALID, "gsp_scale_digest_get: NULL");
     GSP_REQUIRE(t >= 0 && t <= s->tick, GSP_ERR_INVALID, "gsp_scale_digest_get: tick %d", t);
     if (int rc = gsp_scale_sync(s)) return rc;
-    std::vector<unsigned long long> h(size_t(gsp::kDigSlots) * gsp::kDigFields);
-    GSP_HIP(hipMemcpy(h.data(), s->dig.p + size_t(t) * h.size(), h.size() * 8,
-                      hipMemcpyDeviceToHost));
     unsigned long long f[gsp::kDigFields] = {0};
-    for (int sl = 0; sl < gsp::kDigSlots; ++sl)
-        for (int k = 0; k < gsp::kDigFields; ++k) f[k] += h[size_t(sl) * gsp::kDigFields + k];
+    std::vector<unsigned long long> h(size_t(gsp::kDigSlots) * gsp::kDigFields);
+    for (Shard &sh : s->local) {
+        GSP_HIP(hipMemcpy(h.data(), sh.dig.p + size_t(t) * h.size(), h.size() * 8,
+                          hipMemcpyDeviceToHost));
+        for (int sl = 0; sl < gsp::kDigSlots; ++sl)
+            for (int k = 0; k < gsp::kDigFields; ++k) f[k] += h[size_t(sl) * gsp::kDigFields + k];
+    }
     out->tick = t;
     out->node_rounds = int64_t(f[gsp::kDigRounds]);
     out->merges = int64_t(f[gsp::kDigMerges]);
@@ -290,33 +458,39 @@ int gsp_scale_digest_get(gsp_scale *s, int32_t t, gsp_scale_digest *out) {
     return GSP_OK;
 }
 
+// Row r of the current table as seen by this engine: every column held by its shards
+// (the whole row on one GPU or in an in-process group; zeros outside this rank's slice).
 int gsp_scale_row(gsp_scale *s, int32_t r, uint16_t *buf, int32_t cap) {
-    GSP_REQUIRE(s && buf && r >= s->row0 && r < s->row0 + s->rows, GSP_ERR_INVALID,
-                "gsp_scale_row: row %d not on this engine", r);
+    GSP_REQUIRE(s && buf && r >= 0 && r < s->p.n, GSP_ERR_INVALID, "gsp_scale_row: row %d", r);
     GSP_REQUIRE(cap >= s->p.n, GSP_ERR_INVALID, "gsp_scale_row: cap %d < n %d", cap, s->p.n);
     if (int rc = gsp_scale_sync(s)) return rc;
+    std::memset(buf, 0, size_t(s->p.n) * 2);
     // a crashed row stops at its fail tick: read the buffer of the last tick it ran
     const int32_t last = std::min(s->tick, s->h_fail[size_t(r)]);
-    const uint16_t *src = s->table[last & 1].p + size_t(r - s->row0) * size_t(s->stride);
-    GSP_HIP(hipMemcpy(buf, src, size_t(s->p.n) * 2, hipMemcpyDeviceToHost));
+    for (Shard &sh : s->local) {
+        const int64_t c0 = sh.col0;
+        const int64_t cnt = std::min<int64_t>(s->stride, int64_t(s->p.n) - c0);
+        if (cnt <= 0) continue;
+        const uint16_t *src = sh.table[last & 1].p + size_t(r) * size_t(s->stride);
+        GSP_HIP(hipMemcpy(buf + c0, src, size_t(cnt) * 2, hipMemcpyDeviceToHost));
+    }
     return GSP_OK;
 }
 
 int gsp_scale_own_hb(gsp_scale *s, int32_t r, int32_t *hb) {
-    GSP_REQUIRE(s && hb && r >= s->row0 && r < s->row0 + s->rows, GSP_ERR_INVALID,
-                "gsp_scale_own_hb: bad row");
+    GSP_REQUIRE(s && hb && r >= 0 && r < s->p.n, GSP_ERR_INVALID, "gsp_scale_own_hb: bad row");
     if (int rc = gsp_scale_sync(s)) return rc;
-    GSP_HIP(hipMemcpy(hb, s->own_hb.p + (r - s->row0), 4, hipMemcpyDeviceToHost));
+    GSP_HIP(hipMemcpy(hb, s->local[0].own_hb.p + r, 4, hipMemcpyDeviceToHost));
     return GSP_OK;
 }
 
 int gsp_scale_messages(gsp_scale *s, int32_t *dst, int64_t cap, int64_t *n) {
     GSP_REQUIRE(s && n, GSP_ERR_INVALID, "gsp_scale_messages: NULL");
     if (int rc = gsp_scale_sync(s)) return rc;
-    const int64_t slots = int64_t(s->rows) * s->p.fanout;
+    const int64_t slots = int64_t(s->p.n) * s->p.fanout;
     *n = slots;
     if (dst && cap > 0)
-        GSP_HIP(hipMemcpy(dst, s->out_dst.p, size_t(std::min(cap, slots)) * 4,
+        GSP_HIP(hipMemcpy(dst, s->local[0].out_dst.p, size_t(std::min(cap, slots)) * 4,
                           hipMemcpyDeviceToHost));
     return GSP_OK;
 }
@@ -325,14 +499,14 @@ int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out) {
     GSP_REQUIRE(s && out, GSP_ERR_INVALID, "gsp_scale_perf_get: NULL");
     if (int rc = gsp_scale_sync(s)) return rc;
     gsp_scale_digest d{};
-    if (s->tick > 0) {
+    if (s->tick > 0)
         if (int rc = gsp_scale_digest_get(s, s->tick, &d)) return rc;
-    }
-    // algorithmic HBM bytes of the fused kernel at the last tick: every processed row
-    // reads its own row and writes it back (2 * stride * 2 B), reads one sender row per
-    // delivered message (stride * 2 B) and its CSR entry (4 B)
-    s->perf.bytes_per_tick = double(2 * d.node_rounds + d.delivered) * double(s->stride) * 2.0 +
-                             double(d.delivered) * 4.0;
+    // algorithmic HBM bytes of the tick kernel(s) of this engine at the last tick: every
+    // processed row reads its own row and writes it back (2 * stride * 2 B per shard), reads
+    // one sender row per delivered message (stride * 2 B) and its CSR entry (4 B)
+    const double rows = double(2 * d.node_rounds + d.delivered);
+    s->perf.bytes_per_tick = (rows * double(s->stride) * 2.0 + double(d.delivered) * 4.0) *
+                             double(s->local.size());
     *out = s->perf;
     return GSP_OK;
 }
@@ -347,6 +521,20 @@ int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy) {
     GSP_REQUIRE(s && policy >= 0 && policy <= 3, GSP_ERR_INVALID,
                 "gsp_scale_set_cache_policy: policy %d", policy);
     s->policy = policy;
+    return GSP_OK;
+}
+
+int gsp_scale_set_merge(gsp_scale *s, int32_t packed) {
+    GSP_REQUIRE(s, GSP_ERR_INVALID, "gsp_scale_set_merge: NULL");
+    s->merge = packed ? 1 : 0;
+    return GSP_OK;
+}
+
+int gsp_scale_layout(gsp_scale *s, int32_t *shards, int32_t *rank, int64_t *stride) {
+    GSP_REQUIRE(s, GSP_ERR_INVALID, "gsp_scale_layout: NULL");
+    if (shards) *shards = s->shards;
+    if (rank) *rank = s->rank;
+    if (stride) *stride = s->stride;
     return GSP_OK;
 }
 

@@ -1,12 +1,14 @@
 // gossip_protocol_amd/csrc/scale_kernels.hip -- SCALE-mode HIP kernels for gfx950.
 //
-// scale_tick_kernel<false> is the whole per-tick hot path of one receiver row, fused:
+// scale_tick_kernel is the per-tick hot path of one receiver row, fused:
 //   merge   (MP1Node::recvCallBack GOSSIP branch, MP1Node.cpp:234-256) of every message the
 //           row received, in ascending sender order, 8 packed entries per lane per 16-B load;
 //   ops     (MP1Node::nodeLoopOps, MP1Node.cpp:335-348): own heartbeat bump, TREMOVE scan;
 //   events  join/remove detection, counted and hashed (order-independent digest);
-//   send    peer choice by Philox rank-select over the row's presence bitmap in LDS, the
-//           drop draw, and the destination count for next tick's CSR.
+//   send    (one GPU) peer choice by Philox rank-select over the row's presence bitmap in
+//           LDS, the drop draw and the destination count for next tick's CSR; (column
+//           shards) the slice's presence bitmap and count, resolved after an all-gather by
+//           scale_resolve_kernel / scale_finalize_kernel.
 // One 256-lane workgroup per row streams the row in 2048-column chunks: it reads its own
 // row and each sender's row once (16 B per lane, fully coalesced) and writes its row once,
 // so the kernel is HBM-bound at (2 + k) * stride * 2 bytes per row with k messages.
@@ -25,6 +27,7 @@ __device__ inline uint64_t event_mix(uint32_t kind, uint32_t t, uint32_t r, uint
     return z ^ (z >> 31);
 }
 
+// ---- scalar form: one entry at a time ---------------------------------------------------
 // Merge one payload entry v (the sender's) into the receiver's entry e (both packed
 // hb << 5 | ts5, 0 = absent):
 //   present: max-merge, ts = now only on a strict heartbeat increase (MP1Node.cpp:247-251)
@@ -37,10 +40,62 @@ __device__ inline uint32_t merge_entry(uint32_t e, uint32_t v, uint32_t t5, uint
     return e ? upd : add;
 }
 
-__device__ inline uint32_t merge_word(uint32_t e, uint32_t v, uint32_t t5, uint32_t tr) {
+__device__ inline uint32_t merge_word_scalar(uint32_t e, uint32_t v, uint32_t t5, uint32_t tr) {
     const uint32_t lo = merge_entry(e & 0xFFFFu, v & 0xFFFFu, t5, tr);
     const uint32_t hi = merge_entry(e >> 16, v >> 16, t5, tr);
     return lo | (hi << 16);
+}
+
+// ---- packed form: two entries per 32-bit word on the v_pk_*_u16 ALUs --------------------
+// hipcc folds min(sub_sat(a, b), 1) back into compares + selects, so the packed ops are
+// spelled out; every operand is a VGPR and nothing reads EXEC or the memory counters.
+__device__ inline uint32_t pk_max(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ inline uint32_t pk_min(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ inline uint32_t pk_sub(uint32_t a, uint32_t b) {
+    uint32_t r; asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ inline uint32_t pk_subc(uint32_t a, uint32_t b) {   // saturating at 0
+    uint32_t r; asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "v"(b)); return r;
+}
+__device__ inline uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r; asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r;
+}
+__device__ inline uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {   // (m & a) | (~m & b)
+    uint32_t r; asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b)); return r;
+}
+
+struct PackedConsts {
+    uint32_t one, t5x2, t32, tr, trm1, low5, hbmask, zero;
+};
+
+__device__ inline PackedConsts packed_consts(uint32_t t5, uint32_t tr) {
+    PackedConsts c;
+    c.one = 0x00010001u;
+    c.t5x2 = t5 | (t5 << 16);
+    c.t32 = c.t5x2 + 0x00200020u;
+    c.tr = tr | (tr << 16);
+    c.trm1 = (tr - 1) | ((tr - 1) << 16);
+    c.low5 = 0x001F001Fu;
+    c.hbmask = 0xFFE0FFE0u;
+    c.zero = 0u;
+    return c;
+}
+
+// Same function as merge_word_scalar (checked exhaustively over hb in {0..3, 31, 100, 1000,
+// 2046, 2047} x every ts5 x every t5 x tr in {1, 5, 20, 31}):
+//   present e:  m = max(v & hbmask, e); e' = m + (m != e) * t5
+//   absent e:   e' = v if v present and (t5 + 32 - ts5(v)) mod 32 < tr, else 0
+__device__ inline uint32_t merge_word_packed(uint32_t e, uint32_t v, const PackedConsts &c) {
+    const uint32_t m = pk_max(v & c.hbmask, e);
+    const uint32_t rp = pk_mad(pk_min(pk_sub(m, e), c.one), c.t5x2, m);
+    const uint32_t age = (c.t32 - (v & c.low5)) & c.low5;
+    const uint32_t ok = pk_min(pk_subc(c.tr, age), pk_min(v, c.one));
+    const uint32_t ra = v & pk_sub(c.zero, ok);
+    return bfi(pk_sub(c.zero, pk_min(e, c.one)), rp, ra);
 }
 
 // Replace entry i (runtime, 0..7) of a 16-B lane vector.  Only ever reached on the one
@@ -61,19 +116,22 @@ __device__ inline void patch16(uint4 &w, int i, F f) {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 16-byte row accesses; kNT selects the non-temporal (streaming) cache policy
+// 16-byte row accesses; kNT selects the non-temporal (streaming) cache policy.  It must be
+// a compile-time choice: a runtime select between the two forms is CSE'd into one plain load.
 template <bool kNT>
 __device__ inline uint4 ld16(const uint16_t *p) {
     const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
-    const u32x4 v = kNT ? __builtin_nontemporal_load(q) : *q;
+    u32x4 v;
+    if constexpr (kNT) v = __builtin_nontemporal_load(q);
+    else v = *q;
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 template <bool kNT>
-__device__ inline void st16(uint16_t *p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+__device__ inline void st16(uint16_t *p, const uint32_t (&w)[4]) {
     u32x4 v;
-    v.x = a; v.y = b; v.z = c; v.w = d;
+    v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
     u32x4 *q = reinterpret_cast<u32x4 *>(p);
-    if (kNT) __builtin_nontemporal_store(v, q);
+    if constexpr (kNT) __builtin_nontemporal_store(v, q);
     else *q = v;
 }
 
@@ -83,13 +141,62 @@ __device__ inline uint64_t wave_sum_u64(uint64_t v) {
     return v;
 }
 
+// rank-th set bit (0-based) of a bitmap of `words` 32-bit words, by one wave; -1 if none.
+// lane_cnt / pre: this lane's popcount over its words and the exclusive prefix.
+template <typename W>
+__device__ inline int32_t wave_select(W word, int32_t per, uint32_t lane_cnt, uint32_t pre,
+                                      uint32_t rank, int32_t lane) {
+    const bool mine = rank >= pre && rank < pre + lane_cnt;
+    int32_t col = -1;
+    if (mine) {
+        uint32_t m = rank - pre;
+        for (int32_t w = 0; w < per; ++w) {
+            uint32_t bw = word(lane * per + w);
+            const uint32_t pc = __builtin_popcount(bw);
+            if (m < pc) {
+                for (uint32_t q = 0; q < m; ++q) bw &= bw - 1;
+                col = (lane * per + w) * 32 + (__builtin_ffs(bw) - 1);
+                break;
+            }
+            m -= pc;
+        }
+    }
+    const unsigned long long owner = __ballot(mine);
+    if (!owner) return -1;
+    return __shfl(col, __builtin_ffsll(owner) - 1, 64);
+}
+
+__device__ inline uint32_t wave_excl_prefix(uint32_t v, int32_t lane, uint32_t *total) {
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += u;
+    }
+    *total = __shfl(incl, 63, 64);
+    return incl - v;
+}
+
+// Sequential sampling without replacement: draw k maps u % (cnt - k) onto the ranks not
+// chosen yet, in ascending order (chosen[] kept sorted).  Identical in every lane.
+__device__ inline int32_t next_distinct_rank(uint32_t u, int32_t cnt, int32_t k, int32_t *chosen,
+                                             int32_t &nch) {
+    int32_t rk = int32_t(u % uint32_t(cnt - k));
+    int32_t pos = 0;
+    while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
+    for (int32_t q = nch; q > pos; --q) chosen[q] = chosen[q - 1];
+    chosen[pos] = rk;
+    nch++;
+    return rk;
+}
+
 // kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads
-template <bool kInit, int kPolicy>
+template <bool kInit, bool kSlice, int kMerge, int kPolicy>
 __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
     constexpr bool kNtOwn = (kPolicy & 1) != 0, kNtSrc = (kPolicy & 2) != 0;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // stride / 32 words
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // fused: stride/32 words
     __shared__ int32_t s_src[kMaxSegment];
-    __shared__ int32_t s_raw[kMaxSegment];
+    __shared__ int32_t s_slot[kMaxSegment];
     __shared__ unsigned long long s_red[4][4];
 
     const int32_t tid = threadIdx.x;
@@ -100,7 +207,7 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     const int32_t F = a.fanout;
 
     if (t > a.fail_tick[r]) {          // crashed (Application.cpp:186): no recv, no ops, no send
-        if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
+        if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
         return;
     }
 
@@ -110,23 +217,36 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         k = a.off[lr + 1] - o0;
         if (k > kMaxSegment) {
             if (tid == 0) atomicOr(a.err, 1);
-            if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
+            if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
             return;
         }
-        for (int32_t i = tid; i < k; i += kScaleBlock) s_raw[i] = a.csr_src[o0 + i];
+        for (int32_t i = tid; i < k; i += kScaleBlock) s_src[i] = a.csr_src[o0 + i];
         __syncthreads();
         // canonical receipt order: ascending sender (senders are distinct per receiver)
-        for (int32_t i = tid; i < k; i += kScaleBlock) {
-            const int32_t v = s_raw[i];
-            int32_t rank = 0;
-            for (int32_t j = 0; j < k; ++j) rank += s_raw[j] < v;
-            s_src[rank] = v;
+        int32_t rank[kMaxSegment / kScaleBlock], val[kMaxSegment / kScaleBlock],
+            slot[kMaxSegment / kScaleBlock];
+#pragma unroll
+        for (int q = 0; q < kMaxSegment / kScaleBlock; ++q) {
+            const int32_t i = tid + q * kScaleBlock;
+            rank[q] = -1;
+            if (i < k) {
+                val[q] = s_src[i];
+                slot[q] = a.csr_slot ? a.csr_slot[o0 + i] : val[q] - a.row0;
+                int32_t rk = 0;
+                for (int32_t j = 0; j < k; ++j) rk += s_src[j] < val[q];
+                rank[q] = rk;
+            }
         }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < kMaxSegment / kScaleBlock; ++q)
+            if (rank[q] >= 0) { s_src[rank[q]] = val[q]; s_slot[rank[q]] = slot[q]; }
         __syncthreads();
     }
 
     const uint32_t t5 = uint32_t(t) & 31u;
     const uint32_t tr = uint32_t(a.tremove);
+    const PackedConsts pc = packed_consts(t5, tr);
     const int64_t stride = a.stride;
     const uint16_t *own_prev = a.prev + int64_t(lr) * stride;
     uint16_t *own_cur = a.cur + int64_t(lr) * stride;
@@ -134,77 +254,108 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     uint64_t hsum = 0;
 
     for (int64_t c0 = 0; c0 < stride; c0 += kChunk) {
-        const int64_t col0 = c0 + int64_t(tid) * kEntriesPerLane;
-        uint4 e;
-        uint4 e0 = make_uint4(0, 0, 0, 0);
+        const int64_t lc0 = c0 + int64_t(tid) * kEntriesPerLane;   // column in this table
+        const int64_t gc0 = a.col0 + lc0;                            // global column
+        uint32_t ws[4];
+        uint32_t w0[4] = {0u, 0u, 0u, 0u};
         if (kInit) {
             const uint32_t h = uint32_t(a.h0) << 5;
-            uint32_t ws[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int64_t x0 = col0 + 2 * i, x1 = x0 + 1;
+                const int64_t x0 = gc0 + 2 * i, x1 = x0 + 1;
                 const uint32_t lo = (x0 < a.n && x0 != r) ? h : 0u;
                 const uint32_t hi = (x1 < a.n && x1 != r) ? h : 0u;
                 ws[i] = lo | (hi << 16);
             }
-            e = make_uint4(ws[0], ws[1], ws[2], ws[3]);
         } else {
-            e = ld16<kNtOwn>(own_prev + col0);
-            e0 = e;
+            uint4 e = ld16<kNtOwn>(own_prev + lc0);
+            w0[0] = e.x; w0[1] = e.y; w0[2] = e.z; w0[3] = e.w;
             for (int32_t j0 = 0; j0 < k; j0 += 4) {
                 uint4 v[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (j0 + u < k)
-                        v[u] = ld16<kNtSrc>(a.prev + int64_t(s_src[j0 + u] - a.row0) * stride + col0);
+                for (int u = 0; u < 4; ++u) {
+                    if (j0 + u < k) {
+                        const int32_t sl = s_slot[j0 + u];
+                        const uint16_t *row = sl >= 0 ? a.prev + int64_t(sl) * stride
+                                                      : a.remote + int64_t(-sl - 1) * stride;
+                        v[u] = ld16<kNtSrc>(row + lc0);
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (j0 + u >= k) break;
-                    e.x = merge_word(e.x, v[u].x, t5, tr);
-                    e.y = merge_word(e.y, v[u].y, t5, tr);
-                    e.z = merge_word(e.z, v[u].z, t5, tr);
-                    e.w = merge_word(e.w, v[u].w, t5, tr);
+                    if (kMerge == 1) {
+                        e.x = merge_word_packed(e.x, v[u].x, pc);
+                        e.y = merge_word_packed(e.y, v[u].y, pc);
+                        e.z = merge_word_packed(e.z, v[u].z, pc);
+                        e.w = merge_word_packed(e.w, v[u].w, pc);
+                    } else {
+                        e.x = merge_word_scalar(e.x, v[u].x, t5, tr);
+                        e.y = merge_word_scalar(e.y, v[u].y, t5, tr);
+                        e.z = merge_word_scalar(e.z, v[u].z, t5, tr);
+                        e.w = merge_word_scalar(e.w, v[u].w, t5, tr);
+                    }
                     // the sender's own entry: hb + 1 and ts = now, or add (1, now)
                     // (MP1Node.cpp:237-243); the sender's row never holds itself
-                    const int64_t ds = int64_t(s_src[j0 + u]) - col0;
+                    const int64_t ds = int64_t(s_src[j0 + u]) - gc0;
                     if (ds >= 0 && ds < kEntriesPerLane)
                         patch16(e, int(ds), [t5](uint32_t old) { return (((old >> 5) + 1u) << 5) | t5; });
                 }
             }
-            const int64_t dr = int64_t(r) - col0;      // never list yourself (MP1Node.cpp:290)
+            const int64_t dr = int64_t(r) - gc0;      // never list yourself (MP1Node.cpp:290)
             if (dr >= 0 && dr < kEntriesPerLane) patch16(e, int(dr), [](uint32_t) { return 0u; });
+            ws[0] = e.x; ws[1] = e.y; ws[2] = e.z; ws[3] = e.w;
         }
 
+        // TREMOVE scan, events and presence bits of the 8 entries
+        bool slow = !kInit;
         uint32_t bits = 0;
-        uint32_t ws[4] = {e.x, e.y, e.z, e.w};
-        const uint32_t w0[4] = {e0.x, e0.y, e0.z, e0.w};
+        if (kMerge == 1 && !kInit) {
+            uint32_t ev = 0, q = 0;
 #pragma unroll
-        for (int i = 0; i < kEntriesPerLane; ++i) {
-            const int sh = (i & 1) * 16;
-            uint32_t ent = (ws[i >> 1] >> sh) & 0xFFFFu;
-            if (!kInit && ent) {
-                const uint32_t before = (w0[i >> 1] >> sh) & 0xFFFFu;
-                if (((t5 - ent) & 31u) >= tr) {     // TREMOVE scan (MP1Node.cpp:340)
-                    removes++;
-                    hsum += event_mix(2, uint32_t(t), uint32_t(r), uint32_t(col0 + i));
-                    ws[i >> 1] &= ~(0xFFFFu << sh);
-                    ent = 0;
-                } else if (!before) {
-                    joins++;
-                    hsum += event_mix(1, uint32_t(t), uint32_t(r), uint32_t(col0 + i));
-                }
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t pe = pk_min(ws[i], pc.one);
+                const uint32_t age = (pc.t32 - (ws[i] & pc.low5)) & pc.low5;
+                ev |= pk_min(pk_subc(age, pc.trm1), pe);          // present and stale
+                ev |= pk_subc(pe, pk_min(w0[i], pc.one));          // absent before, present now
+                q |= ((pe | (pe >> 15)) & 3u) << (2 * i);
             }
-            bits |= (ent ? 1u : 0u) << i;
+            slow = ev != 0;
+            bits = q;
+        }
+        if (kInit || slow) {
+            bits = 0;
+#pragma unroll
+            for (int i = 0; i < kEntriesPerLane; ++i) {
+                const int sh = (i & 1) * 16;
+                uint32_t ent = (ws[i >> 1] >> sh) & 0xFFFFu;
+                if (!kInit && ent) {
+                    const uint32_t before = (w0[i >> 1] >> sh) & 0xFFFFu;
+                    if (((t5 - ent) & 31u) >= tr) {     // TREMOVE scan (MP1Node.cpp:340)
+                        removes++;
+                        hsum += event_mix(2, uint32_t(t), uint32_t(r), uint32_t(gc0 + i));
+                        ws[i >> 1] &= ~(0xFFFFu << sh);
+                        ent = 0;
+                    } else if (!before) {
+                        joins++;
+                        hsum += event_mix(1, uint32_t(t), uint32_t(r), uint32_t(gc0 + i));
+                    }
+                }
+                bits |= (ent ? 1u : 0u) << i;
+            }
         }
         live += __builtin_popcount(bits);
-        st16<kNtOwn>(own_cur + col0, ws[0], ws[1], ws[2], ws[3]);
-        // presence bitmap: 8 bits per lane -> byte (col0 / 8)
-        reinterpret_cast<uint8_t *>(s_bits)[col0 >> 3] = uint8_t(bits);
+        st16<kNtOwn>(own_cur + lc0, ws);
+        // presence bitmap: 8 bits per lane -> byte (lc0 / 8)
+        if (kSlice)
+            a.bitmap[int64_t(lr) * (stride >> 3) + (lc0 >> 3)] = uint8_t(bits);
+        else
+            reinterpret_cast<uint8_t *>(s_bits)[lc0 >> 3] = uint8_t(bits);
     }
 
     // block reduction: live, joins, removes, hash
-    uint64_t v0 = wave_sum_u64(live), v1 = wave_sum_u64(joins), v2 = wave_sum_u64(removes);
-    uint64_t v3 = wave_sum_u64(hsum);
+    const uint64_t v0 = wave_sum_u64(live), v1 = wave_sum_u64(joins), v2 = wave_sum_u64(removes);
+    const uint64_t v3 = wave_sum_u64(hsum);
     if (lane == 0) { s_red[wave][0] = v0; s_red[wave][1] = v1; s_red[wave][2] = v2; s_red[wave][3] = v3; }
     __syncthreads();
     const uint64_t tot_live = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
@@ -214,30 +365,27 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         a.cnt_cur[r] = int32_t(tot_live);
         if (!kInit) {
             a.own_hb[lr] += 1;
-            unsigned long long merges = 0;
-            for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
-            atomicAdd(&dig[kDigRounds], 1ull);
-            atomicAdd(&dig[kDigMerges], merges);
-            atomicAdd(&dig[kDigDelivered], (unsigned long long)k);
+            if (a.count_rounds) {
+                unsigned long long merges = 0;
+                for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
+                atomicAdd(&dig[kDigRounds], 1ull);
+                atomicAdd(&dig[kDigMerges], merges);
+                atomicAdd(&dig[kDigDelivered], (unsigned long long)k);
+            }
             atomicAdd(&dig[kDigJoins], s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]);
             atomicAdd(&dig[kDigRemoves], s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
             atomicAdd(&dig[kDigHash], s_red[0][3] + s_red[1][3] + s_red[2][3] + s_red[3][3]);
         }
     }
+    if (kSlice) return;
 
     // send: wave 0 picks min(F, live) distinct members by Philox rank-select
     if (wave == 0) {
-        const int32_t words = int32_t(stride >> 5);     // bitmap words
-        const int32_t per = words >> 6;                 // words per lane (stride % 2048 == 0)
+        const int32_t per = int32_t(stride >> 5) >> 6;   // bitmap words per lane
         uint32_t lane_cnt = 0;
         for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(s_bits[lane * per + w]);
-        uint32_t incl = lane_cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t u = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += u;
-        }
-        const uint32_t pre = incl - lane_cnt;
+        uint32_t total = 0;
+        const uint32_t pre = wave_excl_prefix(lane_cnt, lane, &total);
         const int32_t cnt = int32_t(tot_live);
         const int32_t keff = F < cnt ? F : cnt;
         int32_t chosen[16];
@@ -248,30 +396,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             if (kk < keff) {
                 const uint32_t u = draw_u31(kDomainPeer, a.seed, uint32_t(t), uint32_t(r),
                                             uint32_t(kk), 0u);
-                int32_t rk = int32_t(u % uint32_t(cnt - kk));
-                int32_t pos = 0;
-                while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
-                for (int32_t q = nch; q > pos; --q) chosen[q] = chosen[q - 1];
-                chosen[pos] = rk;
-                nch++;
-                const bool mine = uint32_t(rk) >= pre && uint32_t(rk) < pre + lane_cnt;
-                int32_t col = -1;
-                if (mine) {
-                    uint32_t m = uint32_t(rk) - pre;
-                    for (int32_t w = 0; w < per; ++w) {
-                        uint32_t bw = s_bits[lane * per + w];
-                        const uint32_t pc = __builtin_popcount(bw);
-                        if (m < pc) {
-                            for (uint32_t q = 0; q < m; ++q) bw &= bw - 1;
-                            col = (lane * per + w) * 32 + (__builtin_ffs(bw) - 1);
-                            break;
-                        }
-                        m -= pc;
-                    }
-                }
-                const unsigned long long owner = __ballot(mine);
-                const int32_t src_lane = __builtin_ffsll(owner) - 1;
-                dst = __shfl(col, src_lane, 64);
+                const int32_t rk = next_distinct_rank(u, cnt, kk, chosen, nch);
+                dst = wave_select([&](int32_t w) { return s_bits[w]; }, per, lane_cnt, pre,
+                                  uint32_t(rk), lane);
                 sent++;
                 const uint32_t dr = draw_u31(kDomainSend, a.seed, uint32_t(t), uint32_t(r),
                                              uint32_t(dst), 3u);
@@ -287,6 +414,83 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             atomicAdd(&dig[kDigDropped], dropped);
         }
     }
+}
+
+// Column mode: one wave per sender.  The global member order of row s is the shards'
+// slices in ascending column order, so rank rk lives on the first shard whose inclusive
+// prefix of slice counts exceeds rk; that shard resolves the column from its bitmap.
+__global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) {
+    const int32_t lane = threadIdx.x & 63;
+    const int32_t s = int32_t(blockIdx.x) * 4 + int32_t(threadIdx.x >> 6);
+    if (s >= a.n) return;
+    const int32_t F = a.fanout;
+    if (a.tick > a.fail_tick[s]) {
+        if (lane < F) a.picks[int64_t(s) * F + lane] = -1;
+        return;
+    }
+    const uint32_t c = lane < a.shards ? uint32_t(a.cnt_all[int64_t(lane) * a.n + s]) : 0u;
+    uint32_t total = 0;
+    const uint32_t cpre = wave_excl_prefix(c, lane, &total);
+    if (lane == 0) a.cnt_total[s] = int32_t(total);
+    const int32_t cnt = int32_t(total);
+    const int32_t keff = F < cnt ? F : cnt;
+    const int32_t per = int32_t(a.stride >> 5) >> 6;
+    const uint32_t *bm = reinterpret_cast<const uint32_t *>(a.bitmap + int64_t(s) * (a.stride >> 3));
+    bool have_counts = false;
+    uint32_t lane_cnt = 0, pre = 0;
+    int32_t chosen[16];
+    int32_t nch = 0;
+    for (int32_t kk = 0; kk < F; ++kk) {
+        int32_t pick = -1;
+        if (kk < keff) {
+            const uint32_t u = draw_u31(kDomainPeer, a.seed, uint32_t(a.tick), uint32_t(s),
+                                        uint32_t(kk), 0u);
+            const uint32_t rk = uint32_t(next_distinct_rank(u, cnt, kk, chosen, nch));
+            const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
+            const int32_t g = __builtin_ffsll(own) - 1;
+            if (g == a.shard) {
+                if (!have_counts) {
+                    for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);
+                    uint32_t tot = 0;
+                    pre = wave_excl_prefix(lane_cnt, lane, &tot);
+                    have_counts = true;
+                }
+                const uint32_t local = rk - __shfl(cpre, g, 64);
+                const int32_t col = wave_select([&](int32_t w) { return bm[w]; }, per, lane_cnt, pre,
+                                                local, lane);
+                pick = int32_t(int64_t(a.shard) * a.stride + col);
+            }
+        }
+        if (lane == 0) a.picks[int64_t(s) * F + kk] = pick;
+    }
+    if (lane == 0 && a.count_rounds && keff > 0)
+        atomicAdd(&a.dig[(s % kDigSlots) * kDigFields + kDigSent], (unsigned long long)keff);
+}
+
+__global__ void scale_finalize_kernel(ScaleResolveArgs a) {
+    const int64_t slots = int64_t(a.n) * a.fanout;
+    unsigned long long dropped = 0;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < slots;
+         i += int64_t(gridDim.x) * blockDim.x) {
+        int32_t d = a.picks[i];
+        if (d >= 0) {
+            const int32_t s = int32_t(i / a.fanout);
+            const uint32_t dr = draw_u31(kDomainSend, a.seed, uint32_t(a.tick), uint32_t(s),
+                                         uint32_t(d), 3u);
+            if (int32_t(dr % 100u) < a.drop_pct) { dropped++; d = -1; }
+            else atomicAdd(&a.deg[d], 1);
+        }
+        a.out_dst[i] = d;
+    }
+    dropped = wave_sum_u64(dropped);
+    if ((threadIdx.x & 63) == 0 && dropped && a.count_rounds)
+        atomicAdd(&a.dig[(blockIdx.x % kDigSlots) * kDigFields + kDigDropped], dropped);
+}
+
+__global__ void max_into_kernel(int32_t *dst, const int32_t *src, int64_t count) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < count;
+         i += int64_t(gridDim.x) * blockDim.x)
+        dst[i] = max(dst[i], src[i]);
 }
 
 // Exclusive scan of the destination counts, two launches: (1) every 1024-thread block sums
@@ -370,26 +574,67 @@ __global__ void scatter_kernel(const int32_t *out_dst, int64_t slots, int32_t fa
     }
 }
 
+unsigned grid_for(int64_t items, int64_t per_block, int64_t cap) {
+    int64_t b = (items + per_block - 1) / per_block;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return unsigned(b);
+}
+
 }  // namespace
 
-size_t scale_lds_bytes(int64_t stride) { return size_t(stride / 8); }
+size_t scale_lds_bytes(int64_t stride, bool slice) { return slice ? 16 : size_t(stride / 8); }
 
-hipError_t launch_scale_init(const ScaleTickArgs &a, hipStream_t st) {
+hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st) {
     if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((scale_tick_kernel<true, 0>), dim3(a.rows), dim3(kScaleBlock),
-                       scale_lds_bytes(a.stride), st, a);
+    const size_t lds = scale_lds_bytes(a.stride, slice);
+    if (slice)
+        hipLaunchKernelGGL((scale_tick_kernel<true, true, 1, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a);
+    else
+        hipLaunchKernelGGL((scale_tick_kernel<true, false, 1, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a);
     return hipGetLastError();
 }
 
-hipError_t launch_scale_tick(const ScaleTickArgs &a, int policy, hipStream_t st) {
-    if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    const size_t lds = scale_lds_bytes(a.stride);
+template <bool kSlice, int kMerge>
+void launch_tick_policy(const ScaleTickArgs &a, int policy, size_t lds, hipStream_t st) {
+    const dim3 grid(a.rows), block(kScaleBlock);
     switch (policy & 3) {
-        case 0: hipLaunchKernelGGL((scale_tick_kernel<false, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
-        case 1: hipLaunchKernelGGL((scale_tick_kernel<false, 1>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
-        case 2: hipLaunchKernelGGL((scale_tick_kernel<false, 2>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
-        default: hipLaunchKernelGGL((scale_tick_kernel<false, 3>), dim3(a.rows), dim3(kScaleBlock), lds, st, a); break;
+        case 0: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 0>), grid, block, lds, st, a); break;
+        case 1: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1>), grid, block, lds, st, a); break;
+        case 2: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 2>), grid, block, lds, st, a); break;
+        default: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 3>), grid, block, lds, st, a); break;
     }
+}
+
+hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipStream_t st) {
+    if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
+    const size_t lds = scale_lds_bytes(a.stride, slice);
+    const int policy = (a.nt_own ? 1 : 0) | (a.nt_src ? 2 : 0);
+    if (slice) {
+        if (merge == 1) launch_tick_policy<true, 1>(a, policy, lds, st);
+        else launch_tick_policy<true, 0>(a, policy, lds, st);
+    } else {
+        if (merge == 1) launch_tick_policy<false, 1>(a, policy, lds, st);
+        else launch_tick_policy<false, 0>(a, policy, lds, st);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_resolve(const ScaleResolveArgs &a, hipStream_t st) {
+    if (a.stride % kChunk || a.shards < 1 || a.shards > 64 || a.fanout > 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(scale_resolve_kernel, dim3(unsigned((a.n + 3) / 4)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_finalize(const ScaleResolveArgs &a, hipStream_t st) {
+    const int64_t slots = int64_t(a.n) * a.fanout;
+    hipLaunchKernelGGL(scale_finalize_kernel, dim3(grid_for(slots, 256, 4096)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_max_into(int32_t *dst, const int32_t *src, int64_t count, hipStream_t st) {
+    hipLaunchKernelGGL(max_into_kernel, dim3(grid_for(count, 256, 4096)), dim3(256), 0, st, dst, src,
+                       count);
     return hipGetLastError();
 }
 
@@ -404,11 +649,8 @@ hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, in
 
 hipError_t launch_scatter(const int32_t *out_dst, int64_t slots, int32_t fanout, int32_t row0,
                           const int32_t *off, int32_t *fill, int32_t *csr_src, hipStream_t st) {
-    int64_t blocks = (slots + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(scatter_kernel, dim3(unsigned(blocks)), dim3(256), 0, st, out_dst, slots,
-                       fanout, row0, off, fill, csr_src);
+    hipLaunchKernelGGL(scatter_kernel, dim3(grid_for(slots, 256, 4096)), dim3(256), 0, st, out_dst,
+                       slots, fanout, row0, off, fill, csr_src);
     return hipGetLastError();
 }
 

@@ -1,14 +1,16 @@
 // gossip_protocol_amd/csrc/scale_kernels.hpp -- device side of the SCALE engine.
 //
-// HBM layout (full view, V = n columns, stride = n rounded up to 2048 entries):
+// HBM layout (full view, V = n columns):
 //   table[2][rows][stride]  uint16 entries, ping-pong by tick parity:
-//                           entry = hb << 5 | (ts mod 32), 0 = absent; hb in [1, 2047]
-//   own_hb[rows], fail_tick[rows], cnt[2][rows] (member count, by tick parity)
-//   out_dst[rows * fanout]  this tick's messages (dst id or -1) from each sender slot
-//   deg[n], off[n + 1], fill[n], csr_src[n * fanout]   next tick's receiver CSR
+//                           entry = hb << 5 | (ts mod 32), 0 = absent; hb in [1, 2047].
+//                           One GPU: stride = n rounded up to 2048.  Column shard g of G:
+//                           all n rows, columns [col0, col0 + stride), stride = width / G.
+//   own_hb[rows], fail_tick[n], cnt[2][n] (member count by tick parity)
+//   out_dst[rows * fanout]  this tick's messages (dst id or -1) of each sender slot
+//   deg[n], off[n + 1], fill[n], csr_src[n * fanout] (+ csr_slot)  next tick's receiver CSR
 //   dig[ticks][kDigSlots][kDigFields]   sharded per-tick digest accumulators
-// ts is kept modulo 32: every timestamp the protocol ever compares is within 20 ticks
-// of the current tick ("Why 16 bits are exact").
+// ts is kept modulo 32: every timestamp the protocol ever compares is within 20 ticks of
+// the current tick ("Why 16-bit entries are exact").
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -24,39 +26,68 @@ enum : int { kDigRounds = 0, kDigMerges, kDigSent, kDigDropped, kDigDelivered, k
              kDigRemoves, kDigHash, kDigFields };
 
 struct ScaleTickArgs {
-    const uint16_t *prev;        // table of tick t-1
+    const uint16_t *prev;        // table of tick t-1 (this shard's rows x stride)
     uint16_t *cur;               // table of tick t
-    int64_t stride;              // entries per row
-    int32_t n;                   // nodes = columns
-    int32_t row0;                // first global row of this shard (0 on one GPU)
+    const uint16_t *remote;      // row mode: sender rows received from other shards
+    int64_t stride;              // entries per row in this shard's table
+    int32_t n;                   // nodes = global columns
+    int32_t col0;                // first global column of this shard (column mode)
+    int32_t row0;                // first global row of this shard (row mode)
     int32_t rows;                // rows of this shard
     int32_t tick;
     int32_t tremove;
     int32_t fanout;
     int32_t drop_pct;
     int32_t h0;
+    int32_t nt_own, nt_src;      // non-temporal policy of the own-row / sender-row streams
+    int32_t count_rounds;        // this shard adds node-rounds / merges / sends to the digest
     uint64_t seed;
     const int32_t *fail_tick;    // [n] global
     int32_t *own_hb;             // [rows]
     const int32_t *cnt_prev;     // [n] member counts at t-1 (global ids)
-    int32_t *cnt_cur;            // [n]
+    int32_t *cnt_cur;            // [n] (fused: member count; slice: count in this slice)
     const int32_t *off;          // [rows + 1] receiver CSR
     const int32_t *csr_src;      // sender ids
+    const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
     int32_t *out_dst;            // [rows * fanout]
     int32_t *deg;                // [n] messages per destination (atomic)
+    uint8_t *bitmap;             // slice mode: [rows][stride / 8] presence bits
     unsigned long long *dig;     // [kDigSlots][kDigFields] of this tick
     int32_t *err;                // [1] capacity error flag
 };
 
-hipError_t launch_scale_init(const ScaleTickArgs &a, hipStream_t st);
-// policy: cache policy of the row streams (bit 0 own row non-temporal, bit 1 sender rows)
-hipError_t launch_scale_tick(const ScaleTickArgs &a, int policy, hipStream_t st);
+// merge: 0 = per-entry scalar form, 1 = packed 16-bit form (v_pk_* / v_bfi_b32)
+hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st);
+hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipStream_t st);
+
+// Column mode, after the all-gather of every shard's per-row slice counts:
+//   resolve: per sender, Philox rank-select over the global order of its members; the
+//            shard owning the chosen rank resolves the column from its bitmap slice.
+//            picks[s * f + k] = column or -1; cnt_total[s] = member count of s.
+//   finalize (after an all-reduce MAX of picks): drop draw, out_dst, deg.
+struct ScaleResolveArgs {
+    int32_t n, fanout, tick, drop_pct, shard, shards, count_rounds;
+    int64_t stride;              // slice width
+    uint64_t seed;
+    const int32_t *fail_tick;
+    const int32_t *cnt_all;      // [shards][n]
+    int32_t *cnt_total;          // [n]
+    const uint8_t *bitmap;       // [n][stride / 8]
+    int32_t *picks;              // [n * fanout]
+    int32_t *out_dst;            // [n * fanout]
+    int32_t *deg;                // [n]
+    unsigned long long *dig;
+};
+hipError_t launch_scale_resolve(const ScaleResolveArgs &a, hipStream_t st);
+hipError_t launch_scale_finalize(const ScaleResolveArgs &a, hipStream_t st);
+hipError_t launch_max_into(int32_t *dst, const int32_t *src, int64_t count, hipStream_t st);
+
 // off[0..n] = exclusive scan of deg[0..n); tile_sum holds ceil(n / 4096) ints of scratch
 hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, int32_t *tile_sum,
                                  hipStream_t st);
 // csr_src[off[d] + k] = sender, for every message slot i with out_dst[i] = d >= 0
 hipError_t launch_scatter(const int32_t *out_dst, int64_t slots, int32_t fanout, int32_t row0,
                           const int32_t *off, int32_t *fill, int32_t *csr_src, hipStream_t st);
-size_t scale_lds_bytes(int64_t stride);
+size_t scale_lds_bytes(int64_t stride, bool slice);
 
 }  // namespace gsp

@@ -18,17 +18,50 @@ def unpack(entries):
     return present, (e >> 5).astype(np.int32), (e & 31).astype(np.int32)
 
 
+def nccl_unique_id():
+    """RCCL unique id (bytes) for gsp_scale_create_rank; made by rank 0, broadcast by caller."""
+    buf = ctypes.create_string_buffer(128)
+    check(lib().gsp_scale_nccl_id(buf, 128), "gsp_scale_nccl_id")
+    return buf.raw
+
+
 class ScaleEngine:
+    """One scale engine.
+
+    group=G (> 1): G column shards inside this process on `device` (exchange by device
+    copies).  rank/world/nccl_id: this process holds column shard `rank` of `world`
+    (exchange over RCCL).  Default: one GPU, full rows, fused tick kernel.
+    """
+
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
-                 fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0):
+                 fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0, group=1,
+                 rank=0, world=1, nccl_id=None):
         self.params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
                                           h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
                                           fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
         self._h = ctypes.c_void_p()
-        check(lib().gsp_scale_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
-              "gsp_scale_create")
+        if world > 1:
+            idbuf = ctypes.create_string_buffer(nccl_id, 128)
+            check(lib().gsp_scale_create_rank(ctypes.byref(self.params), device, rank, world,
+                                              idbuf, ctypes.byref(self._h)),
+                  "gsp_scale_create_rank")
+        elif group > 1:
+            check(lib().gsp_scale_create_group(ctypes.byref(self.params), device, group,
+                                               ctypes.byref(self._h)), "gsp_scale_create_group")
+        else:
+            check(lib().gsp_scale_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
+                  "gsp_scale_create")
         self.n = n
         self.fanout = fanout
+
+    def layout(self):
+        g, r, s = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        check(lib().gsp_scale_layout(self._h, ctypes.byref(g), ctypes.byref(r), ctypes.byref(s)),
+              "gsp_scale_layout")
+        return g.value, r.value, s.value
+
+    def set_merge(self, packed):
+        check(lib().gsp_scale_set_merge(self._h, int(packed)), "gsp_scale_set_merge")
 
     def close(self):
         if self._h:

@@ -208,8 +208,27 @@ typedef struct {
     double bytes_per_tick;    /* algorithmic HBM bytes of the fused kernel, last tick  */
 } gsp_scale_perf;
 
-/* Single-GPU engine on `device` (rows [0, n)). */
+/* Single-GPU engine on `device` (rows [0, n), full rows, fused tick kernel). */
 int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out);
+
+/* Column-sharded job (DESIGN.md "Multi-GPU").  Shard g of G owns columns
+ * [g * W, (g + 1) * W) of every row (W = n rounded up to 2048 * G, divided by G); per tick
+ * the shards exchange only per-row member counts (all-gather) and the resolved peer
+ * choices (all-reduce MAX).
+ *   gsp_scale_nccl_id      rank 0 makes the RCCL unique id (NCCL_UNIQUE_ID_BYTES = 128);
+ *                          the caller broadcasts it (e.g. torch.distributed) to every rank
+ *   gsp_scale_create_rank  one process per GPU: this process holds shard `rank` of `world`
+ *   gsp_scale_create_group every shard inside this process on one device, exchanged by
+ *                          device copies (the same kernels and protocol, for testing the
+ *                          sharded path on a single GPU)
+ * Results are identical to gsp_scale_create for any number of shards. */
+int gsp_scale_nccl_id(void *out, size_t cap);
+int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
+                          const void *nccl_id, gsp_scale **out);
+int gsp_scale_create_group(const gsp_scale_params *p, int device, int32_t shards,
+                           gsp_scale **out);
+/* shards of the job, first shard index held by this engine, columns per shard */
+int gsp_scale_layout(gsp_scale *s, int32_t *shards, int32_t *rank, int64_t *stride);
 int gsp_scale_destroy(gsp_scale *s);
 /* Advance `ticks` ticks on the device (no host synchronisation inside). */
 int gsp_scale_step(gsp_scale *s, int32_t ticks);
@@ -231,6 +250,9 @@ int gsp_scale_set_timing(gsp_scale *s, int32_t on);
  * and stores of the receiver's own row, bit 1 = non-temporal loads of sender rows.
  * Results are identical for every policy; only speed differs. */
 int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy);
+/* Merge arithmetic: 1 = packed 16-bit (two entries per v_pk_* instruction, default),
+ * 0 = one entry at a time.  Identical results. */
+int gsp_scale_set_merge(gsp_scale *s, int32_t packed);
 /* The hipStream_t (as void*) every launch of this engine is ordered on, so a caller can
  * bracket a timed region with its own HIP events on the same stream. */
 int gsp_scale_hip_stream(gsp_scale *s, void **stream);

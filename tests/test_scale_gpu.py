@@ -35,14 +35,32 @@ def _compare_state(eng, orc, n, rows):
             assert eng.own_hb(r) == orc.own_hb(r), "own hb row %d" % r
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_f%d_d%d_m%d" % c[:4])
-def test_scale_matches_oracle(case):
+VARIANTS = {
+    # name: (column shards in one process, packed merge, cache policy)
+    "fused": (1, 1, 1),
+    "fused_scalar_merge": (1, 0, 0),
+    "fused_nt_all": (1, 1, 3),
+    "columns2": (2, 1, 1),
+    "columns3": (3, 1, 1),
+    "columns4_scalar": (4, 0, 2),
+}
+VARIANT_CASES = [(c, "fused") for c in CASES] + [
+    (CASES[1], "fused_scalar_merge"), (CASES[3], "fused_nt_all"), (CASES[1], "columns2"),
+    (CASES[3], "columns3"), (CASES[4], "columns2"), (CASES[2], "columns4_scalar")]
+
+
+@pytest.mark.parametrize("case,variant", VARIANT_CASES,
+                         ids=lambda x: x if isinstance(x, str) else "n%d_f%d_d%d_m%d" % x[:4])
+def test_scale_matches_oracle(case, variant):
     n, f, drop, mode, ftick, ppm, seed, ticks = case
+    group, packed, policy = VARIANTS[variant]
     orc = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
                       seed=seed)
     rng = np.random.default_rng(seed)
     with ScaleEngine(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
-                     seed=seed, max_ticks=ticks) as eng:
+                     seed=seed, max_ticks=ticks, group=group) as eng:
+        eng.set_merge(packed)
+        eng.set_cache_policy(policy)
         # tick-0 sends (pre-joined bootstrap)
         src, dst = orc.messages()
         m = eng.messages()
@@ -63,6 +81,26 @@ def test_scale_matches_oracle(case):
         _compare_state(eng, orc, n, range(n) if n <= 512 else range(0, n, 61))
         perf = eng.perf()
         assert perf["ticks"] == ticks and perf["merge_ms"] > 0
+
+
+def test_columns_equal_fused_full_size():
+    """Config-3 size: 4 column shards (in-process exchange) give the one-GPU results."""
+    n, ticks = 65536, 14
+    kw = dict(fanout=3, fail_mode=FAIL_RANDOM, fail_tick=10, fail_ppm=10000, seed=0x5EED,
+              max_ticks=ticks)
+    with ScaleEngine(n, **kw) as a:
+        a.step(ticks)
+        da = [a.digest(t) for t in range(1, ticks + 1)]
+        ra = {r: a.row(r) for r in (0, 12345, n - 1)}
+        ma = a.messages()
+    with ScaleEngine(n, group=4, **kw) as b:
+        assert b.layout() == (4, 0, 16384)
+        b.step(ticks)
+        db = [b.digest(t) for t in range(1, ticks + 1)]
+        for r, row in ra.items():
+            assert np.array_equal(b.row(r), row), r
+        assert np.array_equal(b.messages(), ma)
+    assert da == db
 
 
 def test_scale_full_size_properties():
