@@ -303,7 +303,8 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     s->device = device;
     s->shards = shards;
     s->rank = rank;
-    s->sliced = shards > 1;
+    // a communicator always runs the column protocol (with one rank it exercises RCCL alone)
+    s->sliced = shards > 1 || nccl_id != nullptr;
     const int64_t unit = int64_t(gsp::kChunk) * shards;
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
     s->stride = s->width / shards;
@@ -361,7 +362,7 @@ int gsp_scale_nccl_id(void *out, size_t cap) {
 int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
                           const void *nccl_id, gsp_scale **out) {
     GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_scale_create_rank: NULL nccl id");
-    return scale_build(p, device, world, rank, 1, world > 1 ? nccl_id : nullptr, out);
+    return scale_build(p, device, world, rank, 1, nccl_id, out);
 }
 
 int gsp_scale_destroy(gsp_scale *s) {

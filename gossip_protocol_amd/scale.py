@@ -40,7 +40,7 @@ class ScaleEngine:
                                           h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
                                           fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
         self._h = ctypes.c_void_p()
-        if world > 1:
+        if nccl_id is not None:
             idbuf = ctypes.create_string_buffer(nccl_id, 128)
             check(lib().gsp_scale_create_rank(ctypes.byref(self.params), device, rank, world,
                                               idbuf, ctypes.byref(self._h)),

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""A/B the cache policies of the fused tick kernel at BASELINE config 3 (65,536 full view).
+"""A/B variants of the fused tick kernel at BASELINE config 3 (65,536 full view).
 
-Interleaves the policies tick-pair by tick-pair on one engine (same tables, same protocol
-phase) and prints the mean fused-kernel time and achieved algorithmic GB/s per policy.
+Variants = (merge form, cache policy).  They are interleaved tick-pair by tick-pair on one
+engine (same tables, same protocol phase); prints the mean fused-kernel time and achieved
+algorithmic GB/s per variant.
+    python scripts/ab_policy.py [n] [reps]
 """
 import json
 import os
@@ -11,20 +13,23 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine  # noqa: E402
 
+VARIANTS = [("scalar", 0, 0), ("scalar", 0, 1), ("packed", 1, 0), ("packed", 1, 1),
+            ("packed", 1, 3)]
+
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    policies = [0, 1, 2, 3]
-    stride = -(-n // 2048) * 2048
-    res = {p: [0.0, 0.0, 0] for p in policies}
+    res = {v: [0.0, 0.0, 0] for v in VARIANTS}
     with ScaleEngine(n, fanout=3, fail_mode=FAIL_RANDOM, fail_tick=10, fail_ppm=10000,
-                     seed=0x5EED, max_ticks=6 + reps * len(policies) * 2) as eng:
+                     seed=0x5EED, max_ticks=6 + reps * len(VARIANTS) * 2) as eng:
+        stride = eng.layout()[2]
         eng.step(6)
         eng.sync()
         for _ in range(reps):
-            for p in policies:
-                eng.set_cache_policy(p)
+            for v in VARIANTS:
+                eng.set_merge(v[1])
+                eng.set_cache_policy(v[2])
                 before = eng.perf()
                 t0 = eng.tick
                 eng.step(2)
@@ -34,12 +39,13 @@ def main():
                 for t in range(t0 + 1, t0 + 3):
                     d = eng.digest(t)
                     byts += (2.0 * d["node_rounds"] + d["delivered"]) * stride * 2 + d["delivered"] * 4
-                res[p][0] += after["merge_ms"] - before["merge_ms"]
-                res[p][1] += byts
-                res[p][2] += after["merge_launches"] - before["merge_launches"]
+                res[v][0] += after["merge_ms"] - before["merge_ms"]
+                res[v][1] += byts
+                res[v][2] += after["merge_launches"] - before["merge_launches"]
     out = {}
-    for p, (ms, byts, launches) in res.items():
-        out[p] = {"ms_per_launch": ms / launches, "GBps": byts / (ms * 1e-3) / 1e9}
+    for v, (ms, byts, launches) in res.items():
+        out["%s/policy%d" % (v[0], v[2])] = {"ms_per_launch": ms / launches,
+                                             "GBps": byts / (ms * 1e-3) / 1e9}
     print(json.dumps(out))
 
 

@@ -83,6 +83,22 @@ def test_scale_matches_oracle(case, variant):
         assert perf["ticks"] == ticks and perf["merge_ms"] > 0
 
 
+def test_rccl_rank_path_one_rank():
+    """The RCCL code path (ncclCommInitRank, all-gather, all-reduce MAX) with a world of one:
+    a one-rank communicator still runs the column protocol and must match the oracle."""
+    from gossip_protocol_amd.scale import nccl_unique_id
+    n, ticks = 1024, 16
+    orc = ScaleOracle(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5,
+                      fail_ppm=20000, seed=4)
+    with ScaleEngine(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5, fail_ppm=20000,
+                     seed=4, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id()) as eng:
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, t
+        _compare_state(eng, orc, n, range(0, n, 37))
+
+
 def test_columns_equal_fused_full_size():
     """Config-3 size: 4 column shards (in-process exchange) give the one-GPU results."""
     n, ticks = 65536, 14
