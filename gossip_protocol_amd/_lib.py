@@ -58,6 +58,20 @@ class GspScalePerf(ctypes.Structure):
                 ("csr_ms", ctypes.c_double), ("bytes_per_tick", ctypes.c_double)]
 
 
+class GspPviewParams(ctypes.Structure):
+    _fields_ = [("n", c_int32), ("view", c_int32), ("fanout", c_int32), ("inbox", c_int32),
+                ("drop_pct", c_int32), ("tremove", c_int32), ("h0", c_int32),
+                ("fail_mode", c_int32), ("fail_tick", c_int32), ("fail_ppm", c_int32),
+                ("seed", c_uint64), ("max_ticks", c_int32)]
+
+
+class GspPviewDigest(ctypes.Structure):
+    _fields_ = [("tick", c_int64), ("node_rounds", c_int64), ("merges", c_int64),
+                ("sent", c_int64), ("dropped", c_int64), ("delivered", c_int64),
+                ("overflow", c_int64), ("joins", c_int64), ("removes", c_int64),
+                ("evicts", c_int64), ("event_hash", c_uint64)]
+
+
 # name -> (restype, argtypes); every name here must be exported (tests check it)
 SIGNATURES = {
     "gsp_last_error": (ctypes.c_char_p, []),
@@ -108,6 +122,15 @@ SIGNATURES = {
                                               P(ctypes.c_void_p)]),
     "gsp_scale_layout": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), P(c_int64)]),
     "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
+    "gsp_pview_create": (ctypes.c_int, [P(GspPviewParams), ctypes.c_int, P(ctypes.c_void_p)]),
+    "gsp_pview_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_pview_step": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_pview_sync": (ctypes.c_int, [ctypes.c_void_p]),
+    "gsp_pview_digest_get": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspPviewDigest)]),
+    "gsp_pview_row": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_uint64), c_int32, P(c_int32)]),
+    "gsp_pview_own_hb": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
+    "gsp_pview_messages": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int64, P(c_int64)]),
+    "gsp_pview_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
 }
 
 

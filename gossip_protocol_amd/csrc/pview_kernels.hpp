@@ -1,0 +1,45 @@
+// gossip_protocol_amd/csrc/pview_kernels.hpp -- device side of the PARTIAL-VIEW engine.
+//
+// HBM layout (BASELINE config 5: n = 1,048,576 nodes, V = 256):
+//   view[2][rows][V]   uint64 entry = id << 32 | hb << 5 | (ts mod 32); ~0 = empty slot.
+//                      Each row is sorted by id with the empty slots last (2 KB at V = 256).
+//   len[2][n]          entries per row (by tick parity)
+//   own_hb[rows], fail_tick[n], out_dst[rows * fanout], deg/off/fill/csr_src (receiver CSR)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gsp {
+
+constexpr int kPvBlock = 256;
+constexpr int kPvMaxView = 256;       // V <= 256: one entry per lane per list
+constexpr int kPvMaxInbox = 8;        // K <= 8 messages merged per receiver per tick
+constexpr uint64_t kPvEmpty = ~0ull;
+enum : int { kPvRounds = 0, kPvMerges, kPvSent, kPvDropped, kPvDelivered, kPvOverflow,
+             kPvJoins, kPvRemoves, kPvEvicts, kPvHash, kPvFields };
+constexpr int kPvDigSlots = 64;
+
+struct PviewTickArgs {
+    const uint64_t *prev;        // view table of tick t-1 (this shard's rows)
+    uint64_t *cur;               // view table of tick t
+    const uint64_t *remote;      // row mode: sender rows received from other shards
+    int32_t n, view, inbox, fanout, tick, tremove, drop_pct, h0;
+    int32_t row0, rows;
+    uint64_t seed;
+    const int32_t *fail_tick;    // [n]
+    int32_t *own_hb;             // [rows]
+    const int32_t *len_prev;     // [n]
+    int32_t *len_cur;            // [n]
+    const int32_t *off;          // [rows + 1]
+    const int32_t *csr_src;
+    const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
+    int32_t *out_dst;            // [rows * fanout]
+    int32_t *deg;                // [n]
+    unsigned long long *dig;     // [kPvDigSlots][kPvFields] of this tick
+    int32_t *err;
+};
+
+hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st);
+hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st);
+
+}  // namespace gsp

@@ -1,0 +1,77 @@
+"""Python side of the PARTIAL-VIEW engine (gsp_pview_* in include/gossip/gossip.h)."""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+EMPTY = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def unpack_view(entries, length):
+    """(ids, hb, ts mod 32) of the first `length` packed entries."""
+    e = np.asarray(entries, dtype=np.uint64)[:length]
+    ids = (e >> np.uint64(32)).astype(np.int64)
+    p = (e & np.uint64(0xFFFF)).astype(np.int64)
+    return ids, p >> 5, p & 31
+
+
+class PviewEngine:
+    def __init__(self, n, view=256, fanout=3, inbox=8, drop_pct=0, tremove=20, h0=1,
+                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0):
+        self.params = _lib.GspPviewParams(n=n, view=view, fanout=fanout, inbox=inbox,
+                                          drop_pct=drop_pct, tremove=tremove, h0=h0,
+                                          fail_mode=fail_mode, fail_tick=fail_tick,
+                                          fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
+        self._h = ctypes.c_void_p()
+        check(lib().gsp_pview_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
+              "gsp_pview_create")
+        self.n, self.view, self.fanout = n, view, fanout
+
+    def close(self):
+        if self._h:
+            check(lib().gsp_pview_destroy(self._h), "gsp_pview_destroy")
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def step(self, ticks=1):
+        check(lib().gsp_pview_step(self._h, ticks), "gsp_pview_step")
+
+    def sync(self):
+        check(lib().gsp_pview_sync(self._h), "gsp_pview_sync")
+
+    def digest(self, t):
+        d = _lib.GspPviewDigest()
+        check(lib().gsp_pview_digest_get(self._h, t, ctypes.byref(d)), "gsp_pview_digest_get")
+        return {k: getattr(d, k) for k, _ in d._fields_}
+
+    def row(self, r):
+        buf = np.zeros(self.view, np.uint64)
+        ln = ctypes.c_int32()
+        check(lib().gsp_pview_row(self._h, r, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                  self.view, ctypes.byref(ln)), "gsp_pview_row")
+        return buf, ln.value
+
+    def own_hb(self, r):
+        v = ctypes.c_int32()
+        check(lib().gsp_pview_own_hb(self._h, r, ctypes.byref(v)), "gsp_pview_own_hb")
+        return v.value
+
+    def messages(self):
+        n = ctypes.c_int64()
+        check(lib().gsp_pview_messages(self._h, None, 0, ctypes.byref(n)), "gsp_pview_messages")
+        buf = np.zeros(max(n.value, 1), np.int32)
+        check(lib().gsp_pview_messages(self._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                       n.value, ctypes.byref(n)), "gsp_pview_messages")
+        return buf[:n.value].reshape(-1, self.fanout)
+
+    def perf(self):
+        p = _lib.GspScalePerf()
+        check(lib().gsp_pview_perf_get(self._h, ctypes.byref(p)), "gsp_pview_perf_get")
+        return {k: getattr(p, k) for k, _ in p._fields_}

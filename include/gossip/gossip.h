@@ -257,6 +257,36 @@ int gsp_scale_set_merge(gsp_scale *s, int32_t packed);
  * bracket a timed region with its own HIP events on the same stream. */
 int gsp_scale_hip_stream(gsp_scale *s, void **stream);
 
+/* ------------------------------------------------------------------------------------
+ * PARTIAL-VIEW engine (BASELINE config 5): every node keeps at most `view` member entries
+ * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (ascending
+ * sender; the rest are counted as overflow); after the TREMOVE scan a view larger than
+ * `view` keeps the entries with the smallest (age, -hb, id).  DESIGN.md "Partial view".
+ * ---------------------------------------------------------------------------------- */
+typedef struct gsp_pview gsp_pview;
+
+typedef struct {
+    int32_t n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm;
+    uint64_t seed;
+    int32_t max_ticks;
+} gsp_pview_params;
+
+typedef struct {
+    int64_t tick, node_rounds, merges, sent, dropped, delivered, overflow, joins, removes, evicts;
+    uint64_t event_hash;   /* sum of mix64(kind, t, r, x); kinds 1 join, 2 remove, 3 evict */
+} gsp_pview_digest;
+
+int gsp_pview_create(const gsp_pview_params *p, int device, gsp_pview **out);
+int gsp_pview_destroy(gsp_pview *s);
+int gsp_pview_step(gsp_pview *s, int32_t ticks);
+int gsp_pview_sync(gsp_pview *s);
+int gsp_pview_digest_get(gsp_pview *s, int32_t t, gsp_pview_digest *out);
+/* Row r: `view` packed entries (id << 32 | hb << 5 | ts mod 32, ~0 = empty) and its length. */
+int gsp_pview_row(gsp_pview *s, int32_t r, uint64_t *buf, int32_t cap, int32_t *len);
+int gsp_pview_own_hb(gsp_pview *s, int32_t r, int32_t *hb);
+int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
+int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -76,4 +76,32 @@ int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32
 
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x);
 
+/* ---- partial-view scale protocol restatement (pview_oracle.c) ---- */
+typedef struct {
+    int32_t n;          /* nodes                                                    */
+    int32_t view;       /* V: entries kept per node                                 */
+    int32_t fanout;
+    int32_t inbox;      /* K: messages merged per node per tick (rest = overflow)   */
+    int32_t drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm;
+    uint64_t seed;
+} gsp_pview_cfg;
+
+typedef struct {
+    int64_t tick, node_rounds, merges, sent, dropped, delivered, overflow;
+    int64_t joins, removes, evicts;
+    uint64_t event_hash;   /* kinds: 1 join, 2 remove, 3 evict */
+} gsp_pview_digest;
+
+typedef struct gsp_pview_oracle gsp_pview_oracle;
+gsp_pview_oracle *gsp_pview_oracle_create(const gsp_pview_cfg *cfg);
+void gsp_pview_oracle_destroy(gsp_pview_oracle *o);
+int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d);
+/* view of r (ascending id); returns its length */
+int32_t gsp_pview_oracle_row(const gsp_pview_oracle *o, int32_t r, int32_t *id, int32_t *hb,
+                             int32_t *ts);
+int gsp_pview_oracle_own_hb(const gsp_pview_oracle *o, int32_t r);
+int32_t gsp_pview_oracle_fail_tick(const gsp_pview_oracle *o, int32_t r);
+int64_t gsp_pview_oracle_messages(const gsp_pview_oracle *o, int32_t *src, int32_t *dst,
+                                  int64_t cap);
+
 #endif

@@ -1,0 +1,286 @@
+/*
+ * oracle/pview_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * Sequential restatement of the build-defined PARTIAL-VIEW scale protocol (DESIGN.md
+ * "Partial view", BASELINE config 5): every node keeps at most V member entries
+ * (id, hb, ts) sorted by id.  Per-entry rules are the reference's (MP1Node.cpp:234-301,
+ * 335-348) applied per id; the bounded-state choices are the build's:
+ *   init      view of r = {(r + 1 + j * (n / V)) mod n : j < V} (all others if n - 1 <= V),
+ *             hb = h0, ts = 0;
+ *   inbox     a receiver merges at most K messages per tick, in ascending sender order; the
+ *             rest are counted as overflow and ignored;
+ *   evict     after the TREMOVE scan, a view larger than V keeps the V entries with the
+ *             smallest (age, -hb, id);
+ *   send      min(f, |view|) distinct members by Philox rank-select over the id order.
+ * Absolute int32 timestamps (the device stores ts mod 32).
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "gsp_oracle.h"
+#include "gsp_philox.h"
+
+typedef struct { int32_t id, hb, ts; } pv_ent;
+
+struct gsp_pview_oracle {
+    gsp_pview_cfg c;
+    int32_t t;
+    int cur;
+    pv_ent *tab[2];      /* [n][V] */
+    int32_t *len[2];     /* [n] */
+    int32_t *own_hb, *fail_tick;
+    int32_t *msrc, *mdst;
+    int64_t nmsg, mcap;
+};
+
+static int alive_at(const gsp_pview_oracle *o, int32_t r, int32_t t) { return t <= o->fail_tick[r]; }
+
+static void pv_fail_ticks(gsp_pview_oracle *o) {
+    const gsp_pview_cfg *c = &o->c;
+    for (int32_t r = 0; r < c->n; ++r) o->fail_tick[r] = 0x7FFFFFFF;
+    if (c->fail_mode == 1) {
+        for (int32_t r = 0; r < c->n; ++r)
+            if (gsp_philox_u31(GSP_DOMAIN_FAIL, c->seed, (uint32_t)c->fail_tick, (uint32_t)r, 0, 0) %
+                    1000000u < (uint32_t)c->fail_ppm)
+                o->fail_tick[r] = c->fail_tick;
+    } else if (c->fail_mode == 2) {
+        int64_t m = (int64_t)c->n * c->fail_ppm / 1000000;
+        uint32_t start = gsp_philox_u31(GSP_DOMAIN_FAIL, c->seed, (uint32_t)c->fail_tick,
+                                        0xFFFFFFFFu, 0, 0) % (uint32_t)c->n;
+        for (int64_t i = 0; i < m; ++i) o->fail_tick[(start + i) % c->n] = c->fail_tick;
+    }
+}
+
+static const pv_ent *find_id(const pv_ent *l, int32_t len, int32_t id) {
+    int32_t lo = 0, hi = len;
+    while (lo < hi) {
+        int32_t mid = (lo + hi) >> 1;
+        if (l[mid].id < id) lo = mid + 1; else hi = mid;
+    }
+    return (lo < len && l[lo].id == id) ? &l[lo] : NULL;
+}
+
+static void pv_send_all(gsp_pview_oracle *o, int tab, int32_t t, gsp_pview_digest *d) {
+    const gsp_pview_cfg *c = &o->c;
+    o->nmsg = 0;
+    int32_t chosen[64];
+    for (int32_t s = 0; s < c->n; ++s) {
+        if (!alive_at(o, s, t)) continue;
+        const pv_ent *l = o->tab[tab] + (size_t)s * c->view;
+        int32_t cnt = o->len[tab][s];
+        int32_t keff = c->fanout < cnt ? c->fanout : cnt;
+        int32_t nch = 0;
+        for (int32_t k = 0; k < keff; ++k) {
+            uint32_t u = gsp_philox_u31(GSP_DOMAIN_PEER, c->seed, (uint32_t)t, (uint32_t)s,
+                                        (uint32_t)k, 0);
+            int32_t rk = (int32_t)(u % (uint32_t)(cnt - k));
+            int32_t pos = 0;
+            while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
+            memmove(&chosen[pos + 1], &chosen[pos], sizeof(int32_t) * (nch - pos));
+            chosen[pos] = rk;
+            nch++;
+            int32_t dst = l[rk].id;
+            if (d) d->sent++;
+            uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, (uint32_t)s,
+                                         (uint32_t)dst, 3u);
+            if ((int32_t)(dr % 100u) < c->drop_pct) { if (d) d->dropped++; continue; }
+            if (o->nmsg == o->mcap) {
+                o->mcap = o->mcap ? o->mcap * 2 : 1024;
+                o->msrc = realloc(o->msrc, sizeof(int32_t) * o->mcap);
+                o->mdst = realloc(o->mdst, sizeof(int32_t) * o->mcap);
+            }
+            o->msrc[o->nmsg] = s;
+            o->mdst[o->nmsg] = dst;
+            o->nmsg++;
+        }
+    }
+}
+
+gsp_pview_oracle *gsp_pview_oracle_create(const gsp_pview_cfg *cfg) {
+    if (!cfg || cfg->n < 2 || cfg->view < 1 || cfg->fanout < 1 || cfg->fanout > 60 ||
+        cfg->inbox < 1)
+        return NULL;
+    gsp_pview_oracle *o = calloc(1, sizeof *o);
+    o->c = *cfg;
+    const int32_t n = cfg->n, V = cfg->view;
+    for (int b = 0; b < 2; ++b) {
+        o->tab[b] = calloc((size_t)n * V, sizeof(pv_ent));
+        o->len[b] = calloc(n, sizeof(int32_t));
+    }
+    o->own_hb = calloc(n, sizeof(int32_t));
+    o->fail_tick = calloc(n, sizeof(int32_t));
+    pv_fail_ticks(o);
+    for (int32_t r = 0; r < n; ++r) {
+        pv_ent *l = o->tab[0] + (size_t)r * V;
+        int32_t m = 0;
+        if (n - 1 <= V) {
+            for (int32_t x = 0; x < n; ++x)
+                if (x != r) l[m++] = (pv_ent){x, cfg->h0, 0};
+        } else {
+            int32_t stride = n / V;
+            for (int32_t j = 0; j < V; ++j) {
+                int32_t x = (int32_t)(((int64_t)r + 1 + (int64_t)j * stride) % n);
+                l[m++] = (pv_ent){x, cfg->h0, 0};
+            }
+            /* a rotation of an ascending run: sort by id */
+            for (int32_t i = 1; i < m; ++i) {
+                pv_ent v = l[i];
+                int32_t j = i - 1;
+                while (j >= 0 && l[j].id > v.id) { l[j + 1] = l[j]; j--; }
+                l[j + 1] = v;
+            }
+        }
+        o->len[0][r] = m;
+    }
+    o->cur = 0;
+    o->t = 0;
+    pv_send_all(o, 0, 0, NULL);
+    return o;
+}
+
+void gsp_pview_oracle_destroy(gsp_pview_oracle *o) {
+    if (!o) return;
+    for (int b = 0; b < 2; ++b) { free(o->tab[b]); free(o->len[b]); }
+    free(o->own_hb); free(o->fail_tick); free(o->msrc); free(o->mdst);
+    free(o);
+}
+
+static int cmp_i32(const void *a, const void *b) {
+    int32_t x = *(const int32_t *)a, y = *(const int32_t *)b;
+    return (x > y) - (x < y);
+}
+
+typedef struct { pv_ent e; int32_t age; } keyed;
+static int cmp_keep(const void *a, const void *b) {
+    const keyed *x = a, *y = b;
+    if (x->age != y->age) return x->age < y->age ? -1 : 1;
+    if (x->e.hb != y->e.hb) return x->e.hb > y->e.hb ? -1 : 1;
+    return (x->e.id > y->e.id) - (x->e.id < y->e.id);
+}
+static int cmp_id(const void *a, const void *b) {
+    const pv_ent *x = a, *y = b;
+    return (x->id > y->id) - (x->id < y->id);
+}
+
+int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
+    const gsp_pview_cfg *c = &o->c;
+    const int32_t n = c->n, V = c->view, T = c->tremove, K = c->inbox;
+    const int32_t t = o->t + 1;
+    const int prev = o->cur, next = 1 - o->cur;
+    memset(d, 0, sizeof *d);
+    d->tick = t;
+
+    int32_t *deg = calloc((size_t)n + 1, sizeof(int32_t));
+    for (int64_t m = 0; m < o->nmsg; ++m) deg[o->mdst[m] + 1]++;
+    for (int32_t r = 0; r < n; ++r) deg[r + 1] += deg[r];
+    int32_t *fill = calloc(n, sizeof(int32_t));
+    int32_t *bucket = malloc(sizeof(int32_t) * (o->nmsg ? o->nmsg : 1));
+    for (int64_t m = 0; m < o->nmsg; ++m) {
+        int32_t r = o->mdst[m];
+        bucket[deg[r] + fill[r]++] = o->msrc[m];
+    }
+    int32_t *ids = malloc(sizeof(int32_t) * (size_t)(V + (size_t)K * (V + 1) + 1));
+    pv_ent *res = malloc(sizeof(pv_ent) * (size_t)(V + (size_t)K * (V + 1) + 1));
+    keyed *kk = malloc(sizeof(keyed) * (size_t)(V + (size_t)K * (V + 1) + 1));
+
+    for (int32_t r = 0; r < n; ++r) {
+        pv_ent *out = o->tab[next] + (size_t)r * V;
+        const pv_ent *own = o->tab[prev] + (size_t)r * V;
+        const int32_t own_len = o->len[prev][r];
+        if (!alive_at(o, r, t)) {
+            memcpy(out, own, sizeof(pv_ent) * V);
+            o->len[next][r] = own_len;
+            continue;
+        }
+        d->node_rounds++;
+        int32_t *b = bucket + deg[r];
+        int32_t k = deg[r + 1] - deg[r];
+        qsort(b, k, sizeof(int32_t), cmp_i32);
+        if (k > K) { d->overflow += k - K; k = K; }
+        d->delivered += k;
+        /* candidate ids: own view, each sender, each payload */
+        int32_t nid = 0;
+        for (int32_t i = 0; i < own_len; ++i) ids[nid++] = own[i].id;
+        for (int32_t j = 0; j < k; ++j) {
+            int32_t s = b[j];
+            ids[nid++] = s;
+            const pv_ent *pl = o->tab[prev] + (size_t)s * V;
+            for (int32_t i = 0; i < o->len[prev][s]; ++i) ids[nid++] = pl[i].id;
+            d->merges += 1 + o->len[prev][s];
+        }
+        qsort(ids, nid, sizeof(int32_t), cmp_i32);
+        int32_t nres = 0;
+        for (int32_t i = 0; i < nid; ++i) {
+            if (i && ids[i] == ids[i - 1]) continue;
+            const int32_t x = ids[i];
+            const pv_ent *e0 = find_id(own, own_len, x);
+            int present = e0 != NULL;
+            pv_ent cur = e0 ? *e0 : (pv_ent){x, 0, 0};
+            for (int32_t j = 0; j < k; ++j) {
+                const int32_t s = b[j];
+                if (x == s) {                                   /* MP1Node.cpp:237-243 */
+                    if (present) { cur.hb += 1; cur.ts = t; }
+                    else { present = 1; cur.hb = 1; cur.ts = t; }
+                    continue;
+                }
+                const pv_ent *v = find_id(o->tab[prev] + (size_t)s * V, o->len[prev][s], x);
+                if (!v) continue;
+                if (present) {                                  /* MP1Node.cpp:247-251 */
+                    if (v->hb > cur.hb) { cur.hb = v->hb; cur.ts = t; }
+                } else if (x != r && t - v->ts < T) {           /* MP1Node.cpp:282-301 */
+                    present = 1; cur.hb = v->hb; cur.ts = v->ts;
+                }
+            }
+            if (!present) continue;
+            if (!e0) { d->joins++; d->event_hash += gsp_event_mix(1, t, r, x); }
+            if (t - cur.ts >= T) {                              /* MP1Node.cpp:340 */
+                d->removes++; d->event_hash += gsp_event_mix(2, t, r, x);
+                continue;
+            }
+            res[nres++] = cur;
+        }
+        o->own_hb[r] += 1;
+        if (nres > V) {
+            for (int32_t i = 0; i < nres; ++i) { kk[i].e = res[i]; kk[i].age = t - res[i].ts; }
+            qsort(kk, nres, sizeof(keyed), cmp_keep);
+            for (int32_t i = V; i < nres; ++i) {
+                d->evicts++;
+                d->event_hash += gsp_event_mix(3, t, r, kk[i].e.id);
+            }
+            for (int32_t i = 0; i < V; ++i) res[i] = kk[i].e;
+            nres = V;
+            qsort(res, nres, sizeof(pv_ent), cmp_id);
+        }
+        memcpy(out, res, sizeof(pv_ent) * nres);
+        o->len[next][r] = nres;
+    }
+    free(deg); free(fill); free(bucket); free(ids); free(res); free(kk);
+    o->cur = next;
+    o->t = t;
+    pv_send_all(o, next, t, d);
+    return 0;
+}
+
+int32_t gsp_pview_oracle_row(const gsp_pview_oracle *o, int32_t r, int32_t *id, int32_t *hb,
+                             int32_t *ts) {
+    if (r < 0 || r >= o->c.n) return -1;
+    const pv_ent *l = o->tab[o->cur] + (size_t)r * o->c.view;
+    int32_t m = o->len[o->cur][r];
+    for (int32_t i = 0; i < m; ++i) {
+        if (id) id[i] = l[i].id;
+        if (hb) hb[i] = l[i].hb;
+        if (ts) ts[i] = l[i].ts;
+    }
+    return m;
+}
+
+int gsp_pview_oracle_own_hb(const gsp_pview_oracle *o, int32_t r) { return o->own_hb[r]; }
+int32_t gsp_pview_oracle_fail_tick(const gsp_pview_oracle *o, int32_t r) { return o->fail_tick[r]; }
+
+int64_t gsp_pview_oracle_messages(const gsp_pview_oracle *o, int32_t *src, int32_t *dst,
+                                  int64_t cap) {
+    int64_t k = o->nmsg < cap ? o->nmsg : cap;
+    if (src) memcpy(src, o->msrc, sizeof(int32_t) * k);
+    if (dst) memcpy(dst, o->mdst, sizeof(int32_t) * k);
+    return o->nmsg;
+}

@@ -34,6 +34,26 @@ class TickDigest(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class PviewCfg(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("view", ctypes.c_int32), ("fanout", ctypes.c_int32),
+                ("inbox", ctypes.c_int32), ("drop_pct", ctypes.c_int32),
+                ("tremove", ctypes.c_int32), ("h0", ctypes.c_int32), ("fail_mode", ctypes.c_int32),
+                ("fail_tick", ctypes.c_int32), ("fail_ppm", ctypes.c_int32),
+                ("seed", ctypes.c_uint64)]
+
+
+class PviewDigest(ctypes.Structure):
+    _fields_ = [("tick", ctypes.c_int64), ("node_rounds", ctypes.c_int64),
+                ("merges", ctypes.c_int64), ("sent", ctypes.c_int64),
+                ("dropped", ctypes.c_int64), ("delivered", ctypes.c_int64),
+                ("overflow", ctypes.c_int64), ("joins", ctypes.c_int64),
+                ("removes", ctypes.c_int64), ("evicts", ctypes.c_int64),
+                ("event_hash", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _oracle = None
 
 
@@ -64,6 +84,19 @@ def load_oracle():
         L.gsp_scale_oracle_messages.restype = ctypes.c_int64
         L.gsp_event_mix.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
         L.gsp_event_mix.restype = ctypes.c_uint64
+        L.gsp_pview_oracle_create.argtypes = [ctypes.POINTER(PviewCfg)]
+        L.gsp_pview_oracle_create.restype = ctypes.c_void_p
+        L.gsp_pview_oracle_destroy.argtypes = [ctypes.c_void_p]
+        L.gsp_pview_oracle_step.argtypes = [ctypes.c_void_p, ctypes.POINTER(PviewDigest)]
+        L.gsp_pview_oracle_row.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+        L.gsp_pview_oracle_row.restype = ctypes.c_int32
+        L.gsp_pview_oracle_own_hb.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.gsp_pview_oracle_fail_tick.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        L.gsp_pview_oracle_fail_tick.restype = ctypes.c_int32
+        L.gsp_pview_oracle_messages.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int64]
+        L.gsp_pview_oracle_messages.restype = ctypes.c_int64
         _oracle = L
     return _oracle
 
@@ -128,6 +161,54 @@ class ScaleOracle:
     def close(self):
         if self.h:
             self.L.gsp_scale_oracle_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class PviewOracle:
+    """The partial-view restatement (oracle/pview_oracle.c)."""
+
+    def __init__(self, n, view=256, fanout=3, inbox=8, drop_pct=0, tremove=20, h0=1,
+                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED):
+        self.L = load_oracle()
+        self.cfg = PviewCfg(n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick,
+                            fail_ppm, seed)
+        self.h = self.L.gsp_pview_oracle_create(ctypes.byref(self.cfg))
+        assert self.h, "pview oracle create failed"
+        self.n, self.view = n, view
+
+    def step(self):
+        d = PviewDigest()
+        assert self.L.gsp_pview_oracle_step(self.h, ctypes.byref(d)) == 0
+        return d.as_dict()
+
+    def row(self, r):
+        import numpy as np
+        ids = np.zeros(self.view, np.int32)
+        hb = np.zeros(self.view, np.int32)
+        ts = np.zeros(self.view, np.int32)
+        m = self.L.gsp_pview_oracle_row(self.h, r, ids.ctypes.data, hb.ctypes.data, ts.ctypes.data)
+        return ids[:m], hb[:m], ts[:m]
+
+    def own_hb(self, r):
+        return self.L.gsp_pview_oracle_own_hb(self.h, r)
+
+    def fail_tick(self, r):
+        return self.L.gsp_pview_oracle_fail_tick(self.h, r)
+
+    def messages(self):
+        import numpy as np
+        n = self.L.gsp_pview_oracle_messages(self.h, None, None, 0)
+        src = np.zeros(max(n, 1), np.int32)
+        dst = np.zeros(max(n, 1), np.int32)
+        self.L.gsp_pview_oracle_messages(self.h, src.ctypes.data, dst.ctypes.data, n)
+        return src[:n], dst[:n]
+
+    def close(self):
+        if self.h:
+            self.L.gsp_pview_oracle_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -1,0 +1,71 @@
+"""PARTIAL-VIEW engine on the GPU against oracle/pview_oracle.c (BASELINE config 5 rules).
+
+Per tick: every digest field (node-rounds, merges, sends, drops, deliveries, inbox overflow,
+joins, removes, evictions, event hash) identical; periodically the message lists and full
+views (ids and hb exactly, ts mod 32) identical.  Cases cover eviction pressure (small V),
+inbox overflow (small K, large fanout), drops and both failure modes, and views larger
+than the population.
+"""
+import numpy as np
+import pytest
+
+from gossip_protocol_amd.pview import PviewEngine, unpack_view
+from tests.oracle_binding import PviewOracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # n, view, fanout, inbox, drop, fail_mode, fail_tick, ppm, seed, ticks
+    (300, 256, 3, 8, 0, 0, 10, 0, 1, 30),          # V > n - 1: everyone known
+    (2000, 64, 3, 8, 10, 1, 8, 30000, 7, 36),      # eviction every tick
+    (5000, 256, 3, 8, 10, 2, 10, 50000, 11, 22),   # config-5 rules, smaller n
+    (3000, 32, 8, 2, 0, 1, 5, 20000, 3, 30),       # inbox overflow
+    (1500, 100, 5, 4, 30, 2, 6, 100000, 99, 28),   # V not a power of 2
+]
+
+
+def _cmp_rows(eng, orc, rows):
+    for r in rows:
+        ids_o, hb_o, ts_o = orc.row(r)
+        buf, ln = eng.row(r)
+        ids, hb, ts5 = unpack_view(buf, ln)
+        assert ln == len(ids_o), "len row %d: %d vs %d" % (r, ln, len(ids_o))
+        assert np.array_equal(ids, ids_o), "ids row %d" % r
+        assert np.array_equal(hb, hb_o), "hb row %d" % r
+        assert np.array_equal(ts5, ts_o & 31), "ts row %d" % r
+        assert np.all(buf[ln:] == np.uint64(0xFFFFFFFFFFFFFFFF))
+        if orc.fail_tick(r) >= eng_tick(eng):
+            assert eng.own_hb(r) == orc.own_hb(r)
+
+
+def eng_tick(eng):
+    return eng._tick
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d_k%d" % c[:4])
+def test_pview_matches_oracle(case):
+    n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
+    kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+              fail_ppm=ppm, seed=seed)
+    orc = PviewOracle(n, **kw)
+    rng = np.random.default_rng(seed)
+    with PviewEngine(n, max_ticks=ticks, **kw) as eng:
+        eng._tick = 0
+        src, dst = orc.messages()
+        m = eng.messages()
+        assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+            sorted(zip(src.tolist(), dst.tolist()))
+        _cmp_rows(eng, orc, range(0, n, max(1, n // 50)))
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            eng._tick = t
+            got = eng.digest(t)
+            assert got == want, "tick %d\n got %s\nwant %s" % (t, got, want)
+            if t % 5 == 0 or t == ftick + 1:
+                src, dst = orc.messages()
+                m = eng.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+                _cmp_rows(eng, orc, sorted(set(rng.integers(0, n, 40).tolist())))
+        _cmp_rows(eng, orc, range(n) if n <= 2000 else range(0, n, 7))
