@@ -1,29 +1,30 @@
 // gossip_protocol_amd/csrc/pview_kernels.hip -- PARTIAL-VIEW tick kernel for gfx950.
 //
-// One 256-lane workgroup per receiver row, everything in LDS (35 KB):
-//   1. its <= K smallest senders (canonical receipt order, rest = inbox overflow);
-//   2. its own view and the K sender views (each <= V entries, sorted by id), one entry per
-//      lane per list;
-//   3. per-id fold of MP1Node::recvCallBack's rules over the message sequence
-//      (MP1Node.cpp:234-301): every id is handled by the lane holding its FIRST occurrence
-//      (own view, then sender 1, payload 1, sender 2, ...), found with binary searches in the
-//      earlier lists; then the TREMOVE scan (MP1Node.cpp:339-348);
-//   4. union in id order: rank = sum over sources of owned survivors with a smaller id
-//      (per-source prefix counts from one packed block scan);
-//   5. eviction to V by (age, -hb, id): an age histogram, an hb histogram for the boundary
-//      age, an id-order prefix for the last tie -- no sort;
-//   6. the new sorted view is written back; Philox rank-select picks the peers.
-// Bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
+// One 256-lane workgroup per receiver row; the row's work lives in LDS (~41 KB):
+//   1. receipt order: its <= K smallest senders (canonical order; the rest = inbox overflow);
+//   2. keys: its own view and the K sender views, each a sorted block of 256 slots, as
+//      64-bit keys (id << 24 | source << 16 | hb << 5 | ts5); source 0 = own view, j = the
+//      payload of message j, so equal ids sort in message order;
+//   3. union: a tree of merge-path merges (one co-rank binary search per lane per level,
+//      then a short sequential merge): 256 -> 512 -> 1024 -> 2048 keys;
+//   4. fold: the lane holding the first key of an id folds MP1Node::recvCallBack's rules over
+//      that id's run (own entry, sender event j, payload entry j, ...; MP1Node.cpp:234-301)
+//      and runs the TREMOVE test (MP1Node.cpp:339-348); senders found in no list become new
+//      (1, t) entries ("orphans");
+//   5. survivors compacted in id order, orphans merged in; eviction to V by (age, -hb, id)
+//      with an age histogram, an hb histogram of the boundary age and an id-order tie prefix;
+//   6. the new sorted view is written back (2 KB); Philox rank-select picks the peers.
+// HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include "philox.hpp"
 #include "pview_kernels.hpp"
 
 namespace gsp {
 namespace {
 
-constexpr int kLists = 1 + kPvMaxInbox;                   // own view + K payloads
-constexpr int kSrc = kLists + 1;                          // + the sender pseudo-list
-constexpr int kCand = kPvMaxView * kLists + kPvMaxInbox;  // survivors bound (2312)
-constexpr int32_t kNoId = 0x7FFFFFFF;
+constexpr int kSlots = kPvMaxView;                    // slots per source block
+constexpr int kMaxKeys = kSlots * (kPvMaxInbox + 1);  // 2048 with K = 7
+constexpr int kPerLane = kMaxKeys / kPvBlock;          // 8
+constexpr uint64_t kKeyMax = ~0ull;
 
 __device__ inline uint64_t pv_event_mix(uint32_t kind, uint32_t t, uint32_t r, uint32_t x) {
     uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) |
@@ -41,14 +42,11 @@ __device__ inline uint32_t pv_merge(uint32_t e, uint32_t v, uint32_t t5, uint32_
     return e ? upd : add;
 }
 
-__device__ inline int32_t lbound(const int32_t *ids, int32_t len, int32_t x) {
-    int32_t lo = 0, hi = len;
-    while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (ids[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    return lo;
-}
+__device__ inline int32_t key_id(uint64_t k) { return int32_t(k >> 24); }
+__device__ inline uint32_t key_src(uint64_t k) { return uint32_t(k >> 16) & 0xFFu; }
+__device__ inline uint32_t key_val(uint64_t k) { return uint32_t(k) & 0xFFFFu; }
+__device__ inline int32_t ent_id(uint64_t e) { return int32_t(e >> 32); }
+__device__ inline uint32_t ent_val(uint64_t e) { return uint32_t(e) & 0xFFFFu; }
 
 __device__ inline uint64_t wave_sum(uint64_t v) {
 #pragma unroll
@@ -56,55 +54,48 @@ __device__ inline uint64_t wave_sum(uint64_t v) {
     return v;
 }
 
-// exclusive block scan (256 lanes) of W packed words; *total = inclusive sum of all lanes
-template <int W>
-__device__ inline void block_scan_words(uint32_t (&v)[W], uint32_t (&total)[W], uint32_t *s_wave) {
+// exclusive block scan over the 256 lanes (fenced by barriers); *total = sum of all lanes
+__device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_wave) {
     const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t incl[W];
+    uint32_t incl = v;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-        incl[w] = v[w];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t u = __shfl_up(incl[w], d, 64);
-            if (lane >= d) incl[w] += u;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += u;
     }
     __syncthreads();
-    if (lane == 63)
-#pragma unroll
-        for (int w = 0; w < W; ++w) s_wave[wave * W + w] = incl[w];
+    if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
+    uint32_t before = 0, all = 0;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-        uint32_t before = 0, all = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t x = s_wave[q * W + w];
-            before += q < wave ? x : 0u;
-            all += x;
-        }
-        total[w] = all;
-        v[w] = incl[w] - v[w] + before;
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = s_wave[q];
+        before += q < wave ? x : 0u;
+        all += x;
     }
+    *total = all;
+    return incl - v + before;
+}
+
+// number of elements of the ascending array a[0, n) that are < x (by id field)
+__device__ inline int32_t count_ids_below(const uint64_t *a, int32_t n, int32_t x) {
+    int32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (ent_id(a[mid]) < x) lo = mid + 1; else hi = mid;
+    }
+    return lo;
 }
 
 struct PvShared {
-    int32_t ids[kLists][kPvMaxView];     // list ids (kNoId past the end); later: histograms
-    uint16_t val[kLists][kPvMaxView];    // packed hb/ts of the list entries
-    uint8_t flag[kLists][kPvMaxView];    // owned survivor flags
-    uint16_t pre[kSrc][kPvMaxView + 1];  // exclusive prefix of flags per source
-    int32_t oid[kCand];                  // survivors in id order (scratch: raw senders)
-    uint16_t oval[kCand];
-    int32_t src[kPvMaxInbox], slot[kPvMaxInbox], len[kLists];
-    uint8_t sflag[kPvMaxInbox];
-    uint32_t wave_scan[4 * 4];
+    uint64_t keys[2][kMaxKeys];          // ping-pong buffers (32 KB)
+    uint32_t hist[2048];                 // eviction histograms (8 KB)
+    int32_t src[kPvMaxInbox], slot[kPvMaxInbox];
+    int32_t orphan[kPvMaxInbox];         // sender id if it is in no list, else -1
     int32_t misc[8];
-    unsigned long long red[4][6];
+    uint32_t wave_scan[4];
+    unsigned long long red[4][4];
 };
-
-// Packed flag words for the prefix scan: 10-bit fields, 3 per word, sources 0..kSrc-1.
-constexpr int kScanWords = (kSrc + 2) / 3;
 
 template <bool kInit>
 __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
@@ -120,6 +111,8 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
         return;
     }
 
+    // the new view ends up in view_buf as (id << 32 | val), id order
+    const uint64_t *view_buf = sh.keys[0];
     int32_t new_len = 0;
     uint64_t joins = 0, removes = 0, evicts = 0, hsum = 0;
     int32_t k = 0, k_all = 0;
@@ -127,27 +120,26 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
     if (kInit) {
         // pre-joined bounded view: {(r + 1 + j * (n / V)) mod n}, or everyone if n - 1 <= V
         const int32_t n = a.n;
+        const uint64_t h = uint64_t(a.h0) << 5;
         if (n - 1 <= V) {
             for (int32_t x = tid; x < n; x += kPvBlock)
-                if (x != r) { const int32_t p = x < r ? x : x - 1; sh.oid[p] = x; sh.oval[p] = uint16_t(a.h0 << 5); }
+                if (x != r) sh.keys[0][x < r ? x : x - 1] = (uint64_t(x) << 32) | h;
             new_len = n - 1;
         } else {
             const int64_t stride = n / V;
-            const int64_t first_wrap = (int64_t(n) - r - 1 + stride - 1) / stride;   // j that wraps
+            const int64_t first_wrap = (int64_t(n) - r - 1 + stride - 1) / stride;
             const int32_t J = int32_t(first_wrap < V ? first_wrap : V);
-            if (tid < V) {
-                const int32_t j = tid;
+            for (int32_t j = tid; j < V; j += kPvBlock) {
                 int64_t x = int64_t(r) + 1 + int64_t(j) * stride;
                 int32_t p;
                 if (x >= n) { x -= n; p = j - J; } else { p = j + (V - J); }
-                sh.oid[p] = int32_t(x);
-                sh.oval[p] = uint16_t(a.h0 << 5);
+                sh.keys[0][p] = (uint64_t(x) << 32) | h;
             }
             new_len = V;
         }
         __syncthreads();
     } else {
-        // ---- 1. receipt order: the K smallest senders of the segment --------------------
+        // ---- 1. receipt order --------------------------------------------------------------
         const int32_t o0 = a.off[lr];
         k_all = a.off[lr + 1] - o0;
         if (k_all > 1024) {
@@ -155,8 +147,8 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
             if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
             return;
         }
-        int32_t *raw = sh.oid;                       // scratch before the union is built
-        int32_t *raw_slot = &sh.ids[0][0];
+        int32_t *raw = reinterpret_cast<int32_t *>(sh.keys[1]);          // scratch
+        int32_t *raw_slot = raw + 1024;
         for (int32_t i = tid; i < k_all; i += kPvBlock) {
             raw[i] = a.csr_src[o0 + i];
             raw_slot[i] = a.csr_slot ? a.csr_slot[o0 + i] : raw[i] - a.row0;
@@ -170,195 +162,253 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
         }
         __syncthreads();
 
-        // ---- 2. own view and the k sender views into LDS -------------------------------
-        for (int32_t m = 0; m <= k; ++m) {
-            const uint64_t *row;
-            if (m == 0) row = a.prev + int64_t(lr) * V;
-            else {
-                const int32_t sl = sh.slot[m - 1];
-                row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
+        // ---- 2. keys: one sorted block of 256 slots per source ------------------------------
+        int32_t blocks = 1;
+        while (blocks < k + 1) blocks <<= 1;
+        for (int32_t m = 0; m < blocks; ++m) {
+            uint64_t key = kKeyMax;
+            if (m <= k && tid < V) {
+                const uint64_t *row;
+                if (m == 0) row = a.prev + int64_t(lr) * V;
+                else {
+                    const int32_t sl = sh.slot[m - 1];
+                    row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
+                }
+                const uint64_t ent = row[tid];
+                if (ent != kPvEmpty)
+                    key = ((ent >> 32) << 24) | (uint64_t(m) << 16) | (ent & 0xFFFFu);
             }
-            if (tid < kPvMaxView) {
-                const uint64_t ent = tid < V ? row[tid] : kPvEmpty;
-                sh.ids[m][tid] = ent == kPvEmpty ? kNoId : int32_t(ent >> 32);
-                sh.val[m][tid] = ent == kPvEmpty ? 0 : uint16_t(ent & 0xFFFFu);
-            }
-            if (tid == 0) sh.len[m] = m == 0 ? a.len_prev[r] : a.len_prev[sh.src[m - 1]];
+            sh.keys[0][m * kSlots + tid] = key;
         }
-        for (int32_t m = 0; m < kLists; ++m)
-            if (tid < kPvMaxView) sh.flag[m][tid] = 0;
-        if (tid < kPvMaxInbox) sh.sflag[tid] = 0;
         __syncthreads();
 
-        // ---- 3. per-id fold over the message sequence, by the first occurrence ---------
-        // lane `tid` handles entry tid of every list, and sender tid+1 when tid < k
-        uint32_t fin[kSrc];
-        for (int q = 0; q < kSrc; ++q) fin[q] = 0;
+        // ---- 3. merge-path tree: sorted union of every source, ties in message order --------
+        const int32_t P = blocks * kSlots;
+        const int32_t q = P / kPvBlock;                       // keys per lane
+        int32_t cur = 0;
+        for (int32_t s = kSlots; s < P; s <<= 1) {
+            const uint64_t *X = sh.keys[cur];
+            uint64_t *Y = sh.keys[cur ^ 1];
+            const int32_t beg = tid * q;
+            const int32_t b = beg / (2 * s);
+            const int32_t o = beg - b * 2 * s;
+            const uint64_t *A = X + b * 2 * s, *B = A + s;
+            int32_t lo = o > s ? o - s : 0, hi = o < s ? o : s;
+            while (lo < hi) {                                  // co-rank of output o
+                const int32_t mid = (lo + hi) >> 1;
+                if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
+            }
+            int32_t i = lo, j = o - lo;
+            uint64_t *dst = Y + b * 2 * s + o;
+            for (int32_t e = 0; e < q; ++e) {
+                const uint64_t va = i < s ? A[i] : kKeyMax;
+                const uint64_t vb = j < s ? B[j] : kKeyMax;
+                const bool ta = j >= s || (i < s && va < vb);
+                dst[e] = ta ? va : vb;
+                i += ta ? 1 : 0;
+                j += ta ? 0 : 1;
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+        const uint64_t *C = sh.keys[cur];
+
+        // ---- 4. fold each id's run ----------------------------------------------------------
+        const int32_t beg = tid * q;
+        uint32_t res[kPerLane];
+        int32_t rid[kPerLane];
+        uint32_t nloc = 0;
 #pragma unroll
-        for (int q = 0; q < kSrc; ++q) {
-            // q in [0, kLists): list q entry tid;  q == kLists: sender pseudo-entry tid + 1
-            const bool is_sender = q == kLists;
-            const int32_t j = is_sender ? tid + 1 : q;          // message index (0 = own view)
-            if (j > k) continue;
-            if (!is_sender && tid >= sh.len[q]) continue;
-            const int32_t x = is_sender ? sh.src[tid] : sh.ids[q][tid];
-            if (x == r) continue;                                // never list yourself
-            bool owned = true;
-            int32_t p0 = -1;
-            if (j > 0 || is_sender) {
-                p0 = lbound(sh.ids[0], sh.len[0], x);
-                owned = !(p0 < sh.len[0] && sh.ids[0][p0] == x);
-                for (int32_t jj = 1; owned && jj < j; ++jj) {
-                    if (sh.src[jj - 1] == x) { owned = false; break; }
-                    const int32_t p = lbound(sh.ids[jj], sh.len[jj], x);
-                    if (p < sh.len[jj] && sh.ids[jj][p] == x) owned = false;
-                }
-            }
-            if (!owned) continue;
-            const uint32_t e0 = (j == 0 && !is_sender) ? sh.val[0][tid] : 0u;
-            uint32_t cur = e0;
+        for (int32_t e = 0; e < kPerLane; ++e) {
+            res[e] = 0;
+            rid[e] = 0;
+            if (e >= q) continue;
+            const int32_t p = beg + e;
+            const uint64_t key = C[p];
+            if (key == kKeyMax) continue;
+            const int32_t x = key_id(key);
+            if (p > 0 && key_id(C[p - 1]) == x) continue;      // not the first key of its run
+            if (x == r) continue;                              // never list yourself
+            int32_t pos = p;
+            uint32_t e0 = 0;
+            if (key_src(key) == 0) { e0 = key_val(key); pos++; }
+            uint32_t v = e0;
             for (int32_t jj = 1; jj <= k; ++jj) {
-                if (sh.src[jj - 1] == x) {                       // sender entry, MP1Node.cpp:237-243
-                    cur = (((cur >> 5) + 1u) << 5) | t5;
-                    continue;
+                if (sh.src[jj - 1] == x) v = (((v >> 5) + 1u) << 5) | t5;   // MP1Node.cpp:237-243
+                if (pos < P) {
+                    const uint64_t kk = C[pos];
+                    if (key_id(kk) == x && key_src(kk) == uint32_t(jj)) {
+                        v = pv_merge(v, key_val(kk), t5, tr);                 // MP1Node.cpp:247-301
+                        pos++;
+                    }
                 }
-                if (jj < j) continue;                            // x is absent from earlier payloads
-                const int32_t p = lbound(sh.ids[jj], sh.len[jj], x);
-                if (p < sh.len[jj] && sh.ids[jj][p] == x) cur = pv_merge(cur, sh.val[jj][p], t5, tr);
             }
-            if (!cur) continue;
+            if (!v) continue;
             if (!e0) { joins++; hsum += pv_event_mix(1, uint32_t(t), uint32_t(r), uint32_t(x)); }
-            if (((t5 - cur) & 31u) >= tr) {                      // TREMOVE scan
+            if (((t5 - v) & 31u) >= tr) {                      // TREMOVE scan
                 removes++;
                 hsum += pv_event_mix(2, uint32_t(t), uint32_t(r), uint32_t(x));
                 continue;
             }
-            fin[q] = cur;
-            if (is_sender) sh.sflag[tid] = 1; else sh.flag[q][tid] = 1;
+            res[e] = v;
+            rid[e] = x;
+            nloc++;
         }
-        __syncthreads();
-
-        // ---- 4. union in id order -------------------------------------------------------
-        uint32_t words[kScanWords], totw[kScanWords];
-#pragma unroll
-        for (int w = 0; w < kScanWords; ++w) words[w] = 0;
-#pragma unroll
-        for (int q = 0; q < kSrc; ++q) {
-            uint32_t f = 0;
-            if (q < kLists) f = (tid < kPvMaxView) ? sh.flag[q][tid] : 0u;
-            else f = tid < kPvMaxInbox ? sh.sflag[tid] : 0u;
-            words[q / 3] |= f << (10 * (q % 3));
-        }
-        block_scan_words<kScanWords>(words, totw, sh.wave_scan);
-        if (tid < kPvMaxView) {
-#pragma unroll
-            for (int q = 0; q < kSrc; ++q) sh.pre[q][tid] = uint16_t((words[q / 3] >> (10 * (q % 3))) & 1023u);
-        }
-        if (tid == 0) {
-#pragma unroll
-            for (int q = 0; q < kSrc; ++q) sh.pre[q][kPvMaxView] = uint16_t((totw[q / 3] >> (10 * (q % 3))) & 1023u);
-        }
-        int32_t total = 0;
-#pragma unroll
-        for (int q = 0; q < kSrc; ++q) total += int32_t((totw[q / 3] >> (10 * (q % 3))) & 1023u);
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < kSrc; ++q) {
-            if (!fin[q]) continue;
-            const bool is_sender = q == kLists;
-            const int32_t x = is_sender ? sh.src[tid] : sh.ids[q][tid];
-            int32_t rank = 0;
-            for (int32_t m = 0; m <= k; ++m) {
-                const int32_t p = lbound(sh.ids[m], sh.len[m], x);
-                rank += sh.pre[m][p];
+        // senders that are in no list: their sender event is their only event -> (1, t)
+        if (tid < k) {
+            const int32_t x = sh.src[tid];
+            int32_t lo = 0, hi = P;
+            const uint64_t probe = uint64_t(uint32_t(x)) << 24;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi) >> 1;
+                if (C[mid] < probe) lo = mid + 1; else hi = mid;
             }
-            int32_t ps = 0;
-            while (ps < k && sh.src[ps] < x) ps++;
-            rank += sh.pre[kLists][ps];
-            sh.oid[rank] = x;
-            sh.oval[rank] = uint16_t(fin[q]);
+            const bool found = lo < P && C[lo] != kKeyMax && key_id(C[lo]) == x;
+            sh.orphan[tid] = found ? -1 : x;
+            if (!found) { joins++; hsum += pv_event_mix(1, uint32_t(t), uint32_t(r), uint32_t(x)); }
+        }
+        // ---- 5a. survivors, compacted in id order into the other buffer ---------------------
+        uint32_t n_surv = 0;
+        const uint32_t base = block_scan(nloc, &n_surv, sh.wave_scan);   // fences C reads
+        uint64_t *S = sh.keys[cur ^ 1];
+        {
+            uint32_t w = base;
+#pragma unroll
+            for (int32_t e = 0; e < kPerLane; ++e)
+                if (res[e]) S[w++] = (uint64_t(uint32_t(rid[e])) << 32) | res[e];
         }
         __syncthreads();
-
-        // ---- 5. eviction to V by (age, -hb, id) -----------------------------------------
+        // ---- 5b. merge the (<= K, ascending) orphans in: into buffer `cur` (C is done) ------
+        int32_t n_orph = 0;
+        for (int32_t jj = 0; jj < k; ++jj) n_orph += sh.orphan[jj] >= 0 ? 1 : 0;
+        uint64_t *U = sh.keys[cur];
+        const int32_t total = int32_t(n_surv) + n_orph;
+        for (int32_t i = tid; i < int32_t(n_surv); i += kPvBlock) {
+            const uint64_t ent = S[i];
+            int32_t shift = 0;
+            for (int32_t jj = 0; jj < k; ++jj) {
+                const int32_t o = sh.orphan[jj];
+                shift += (o >= 0 && o < ent_id(ent)) ? 1 : 0;
+            }
+            U[i + shift] = ent;
+        }
+        if (tid < k && sh.orphan[tid] >= 0) {
+            const int32_t x = sh.orphan[tid];
+            int32_t below = 0;
+            for (int32_t jj = 0; jj < tid; ++jj) below += sh.orphan[jj] >= 0 ? 1 : 0;  // ascending
+            const int32_t pos = count_ids_below(S, int32_t(n_surv), x) + below;
+            U[pos] = (uint64_t(uint32_t(x)) << 32) | ((1u << 5) | t5);
+        }
+        __syncthreads();
+        view_buf = U;
         new_len = total;
+
+        // ---- 5c. eviction to V by (age, -hb, id) --------------------------------------------
         if (total > V) {
-            int32_t *hist = &sh.ids[0][0];                       // lists are no longer needed
-            for (int32_t i = tid; i < 2048; i += kPvBlock) hist[i] = 0;
+            for (int32_t i = tid; i < 2048; i += kPvBlock) sh.hist[i] = 0;
             __syncthreads();
             for (int32_t i = tid; i < total; i += kPvBlock)
-                atomicAdd(&hist[(t5 - sh.oval[i]) & 31u], 1);
+                atomicAdd(&sh.hist[(t5 - ent_val(U[i])) & 31u], 1u);
             __syncthreads();
-            if (tid == 0) {
-                int32_t cum = 0, ab = 0;
-                for (ab = 0; ab < 32; ++ab) {
-                    if (cum + hist[ab] >= V) break;
-                    cum += hist[ab];
+            if (wave == 0) {                                   // boundary age: first cum >= V
+                const uint32_t hv = lane < 32 ? sh.hist[lane] : 0u;
+                uint32_t incl = hv;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t u = __shfl_up(incl, d, 64);
+                    if (lane >= d) incl += u;
                 }
-                sh.misc[0] = ab;
-                sh.misc[1] = V - cum;                            // kept at the boundary age
-                sh.misc[2] = hist[ab];
+                const unsigned long long hit = __ballot(lane < 32 && incl >= uint32_t(V));
+                const int32_t ab = __builtin_ffsll(hit) - 1;
+                const uint32_t before = __shfl(incl - hv, ab, 64);
+                if (lane == 0) {
+                    sh.misc[0] = ab;
+                    sh.misc[1] = V - int32_t(before);          // kept at the boundary age
+                    sh.misc[2] = int32_t(sh.hist[ab]);
+                }
             }
             __syncthreads();
             const uint32_t astar = uint32_t(sh.misc[0]);
             const int32_t need = sh.misc[1];
             const bool tie = sh.misc[2] > need;
-            uint32_t hstar = 0;
-            int32_t need2 = 0;
-            if (tie) {
-                for (int32_t i = tid; i < 2048; i += kPvBlock) hist[i] = 0;
+            if (tie) {                                         // boundary hb among age == astar
+                for (int32_t i = tid; i < 2048; i += kPvBlock) sh.hist[i] = 0;
                 __syncthreads();
-                for (int32_t i = tid; i < total; i += kPvBlock)
-                    if (((t5 - sh.oval[i]) & 31u) == astar) atomicAdd(&hist[sh.oval[i] >> 5], 1);
+                for (int32_t i = tid; i < total; i += kPvBlock) {
+                    const uint32_t v = ent_val(U[i]);
+                    if (((t5 - v) & 31u) == astar) atomicAdd(&sh.hist[v >> 5], 1u);
+                }
                 __syncthreads();
-                if (tid == 0) {
-                    int32_t cum = 0, h;
-                    for (h = 2047; h > 0; --h) {
-                        if (cum + hist[h] >= need) break;
-                        cum += hist[h];
+                // lane t owns hb bins 2047 - 8t - 7 .. 2047 - 8t (descending order of lanes)
+                uint32_t loc = 0;
+#pragma unroll
+                for (int b = 0; b < 8; ++b) loc += sh.hist[2047 - 8 * tid - b];
+                uint32_t tot = 0;
+                const uint32_t ex = block_scan(loc, &tot, sh.wave_scan);
+                if (ex < uint32_t(need) && uint32_t(need) <= ex + loc) {
+                    uint32_t cum = ex;
+                    for (int b = 0; b < 8; ++b) {
+                        const int32_t h = 2047 - 8 * tid - b;
+                        if (cum + sh.hist[h] >= uint32_t(need)) {
+                            sh.misc[3] = h;
+                            sh.misc[4] = need - int32_t(cum);  // kept among (astar, h) ties
+                            break;
+                        }
+                        cum += sh.hist[h];
                     }
-                    sh.misc[3] = h;
-                    sh.misc[4] = need - cum;                     // kept among (astar, h) ties
                 }
                 __syncthreads();
-                hstar = uint32_t(sh.misc[3]);
-                need2 = sh.misc[4];
             }
-            // keep flags and compaction in id order, chunk by chunk
-            int32_t kept = 0, ties = 0;
-            for (int32_t c0 = 0; c0 < total; c0 += kPvBlock) {
-                const int32_t i = c0 + tid;
-                int32_t x = 0;
-                uint32_t v = 0, keep = 0, istie = 0;
-                if (i < total) {
-                    x = sh.oid[i];
-                    v = sh.oval[i];
-                    const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
-                    istie = tie && age == astar && hb == hstar;
-                    keep = age < astar || (age == astar && (!tie || hb > hstar));
+            const uint32_t hstar = tie ? uint32_t(sh.misc[3]) : 0u;
+            const int32_t need2 = tie ? sh.misc[4] : 0;
+            // contiguous ranges per lane keep the id order for the tie prefix and compaction
+            const int32_t per = (total + kPvBlock - 1) / kPvBlock;
+            const int32_t b0 = tid * per;
+            uint32_t nt = 0;
+            for (int32_t e = 0; e < per; ++e) {
+                const int32_t i = b0 + e;
+                if (i >= total) break;
+                const uint32_t v = ent_val(U[i]);
+                nt += (tie && ((t5 - v) & 31u) == astar && (v >> 5) == hstar) ? 1u : 0u;
+            }
+            uint32_t ntot = 0;
+            uint32_t tie_before = block_scan(nt, &ntot, sh.wave_scan);
+            uint32_t keep_cnt = 0;
+            uint32_t keep_mask = 0;                            // per <= 9 entries of this lane
+            for (int32_t e = 0; e < per; ++e) {
+                const int32_t i = b0 + e;
+                if (i >= total) break;
+                const uint64_t ent = U[i];
+                const uint32_t v = ent_val(ent), age = (t5 - v) & 31u, hb = v >> 5;
+                bool keep = age < astar || (age == astar && (!tie || hb > hstar));
+                if (tie && age == astar && hb == hstar) {
+                    keep = int32_t(tie_before) < need2;
+                    tie_before++;
                 }
-                uint32_t w2[2] = {istie, 0u}, tot2[2];
-                block_scan_words<2>(w2, tot2, sh.wave_scan);
-                if (istie && int32_t(w2[0]) + ties < need2) keep = 1;
-                ties += int32_t(tot2[0]);
-                if (i < total && !keep) {
+                if (keep) { keep_mask |= 1u << e; keep_cnt++; }
+                else {
                     evicts++;
-                    hsum += pv_event_mix(3, uint32_t(t), uint32_t(r), uint32_t(x));
+                    hsum += pv_event_mix(3, uint32_t(t), uint32_t(r), uint32_t(ent_id(ent)));
                 }
-                uint32_t w3[2] = {keep, 0u}, tot3[2];
-                block_scan_words<2>(w3, tot3, sh.wave_scan);   // its barriers fence the reads
-                if (keep) { sh.oid[kept + int32_t(w3[0])] = x; sh.oval[kept + int32_t(w3[0])] = uint16_t(v); }
-                kept += int32_t(tot3[0]);
-                __syncthreads();
             }
-            new_len = kept;
+            uint32_t kept = 0;
+            const uint32_t kbase = block_scan(keep_cnt, &kept, sh.wave_scan);
+            uint64_t *W = sh.keys[cur ^ 1];
+            uint32_t w = kbase;
+            for (int32_t e = 0; e < per; ++e) {
+                const int32_t i = b0 + e;
+                if (i >= total) break;
+                if (keep_mask & (1u << e)) W[w++] = U[i];
+            }
+            __syncthreads();
+            view_buf = W;
+            new_len = int32_t(kept);
         }
     }
 
     // ---- 6. write the new view; heartbeat; send ------------------------------------------
     uint64_t *out = a.cur + int64_t(lr) * V;
-    for (int32_t i = tid; i < V; i += kPvBlock)
-        out[i] = i < new_len ? ((uint64_t(uint32_t(sh.oid[i])) << 32) | sh.oval[i]) : kPvEmpty;
+    for (int32_t i = tid; i < V; i += kPvBlock) out[i] = i < new_len ? view_buf[i] : kPvEmpty;
 
     const uint64_t r0 = wave_sum(joins), r1 = wave_sum(removes), r2 = wave_sum(evicts), r3 = wave_sum(hsum);
     if (lane == 0) { sh.red[wave][0] = r0; sh.red[wave][1] = r1; sh.red[wave][2] = r2; sh.red[wave][3] = r3; }
@@ -392,10 +442,10 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
                 int32_t rk = int32_t(u % uint32_t(new_len - kk));
                 int32_t pos = 0;
                 while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
-                for (int32_t q = nch; q > pos; --q) chosen[q] = chosen[q - 1];
+                for (int32_t q2 = nch; q2 > pos; --q2) chosen[q2] = chosen[q2 - 1];
                 chosen[pos] = rk;
                 nch++;
-                dst = sh.oid[rk];
+                dst = ent_id(view_buf[rk]);
                 sent++;
                 const uint32_t dr = draw_u31(kDomainSend, a.seed, uint32_t(t), uint32_t(r),
                                              uint32_t(dst), 3u);

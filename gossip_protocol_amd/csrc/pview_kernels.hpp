@@ -13,7 +13,7 @@ namespace gsp {
 
 constexpr int kPvBlock = 256;
 constexpr int kPvMaxView = 256;       // V <= 256: one entry per lane per list
-constexpr int kPvMaxInbox = 8;        // K <= 8 messages merged per receiver per tick
+constexpr int kPvMaxInbox = 7;        // K <= 7 messages merged per receiver per tick
 constexpr uint64_t kPvEmpty = ~0ull;
 enum : int { kPvRounds = 0, kPvMerges, kPvSent, kPvDropped, kPvDelivered, kPvOverflow,
              kPvJoins, kPvRemoves, kPvEvicts, kPvHash, kPvFields };

@@ -18,7 +18,7 @@ def unpack_view(entries, length):
 
 
 class PviewEngine:
-    def __init__(self, n, view=256, fanout=3, inbox=8, drop_pct=0, tremove=20, h0=1,
+    def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
                  fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0):
         self.params = _lib.GspPviewParams(n=n, view=view, fanout=fanout, inbox=inbox,
                                           drop_pct=drop_pct, tremove=tremove, h0=h0,

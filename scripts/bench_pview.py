@@ -3,7 +3,7 @@
 
     python scripts/bench_pview.py [--nodes 1048576] [--steps K] [--warmup W]
 
-1,048,576 nodes, V = 256 entries per view (8 B each), fanout 3, inbox 8, 10% drops, a 5%
+1,048,576 nodes, V = 256 entries per view (8 B each), fanout 3, inbox 7, 10% drops, a 5%
 contiguous crash at t = 10.  Algorithmic bytes per node-round: own view read + write
 (2 * V * 8) + one sender view per merged message (V * 8) + 4 B per CSR entry.
 The CPU baseline is oracle/pview_oracle.c (1 thread) on n = 5000 with the same V, fanout,
@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0
-KW = dict(view=256, fanout=3, inbox=8, drop_pct=10, fail_mode=2, fail_tick=10, fail_ppm=50000,
+KW = dict(view=256, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=10, fail_ppm=50000,
           seed=0x5EED)
 
 

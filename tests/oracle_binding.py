@@ -170,7 +170,7 @@ class ScaleOracle:
 class PviewOracle:
     """The partial-view restatement (oracle/pview_oracle.c)."""
 
-    def __init__(self, n, view=256, fanout=3, inbox=8, drop_pct=0, tremove=20, h0=1,
+    def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
                  fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED):
         self.L = load_oracle()
         self.cfg = PviewCfg(n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick,

@@ -16,9 +16,9 @@ pytestmark = pytest.mark.gpu
 
 CASES = [
     # n, view, fanout, inbox, drop, fail_mode, fail_tick, ppm, seed, ticks
-    (300, 256, 3, 8, 0, 0, 10, 0, 1, 30),          # V > n - 1: everyone known
-    (2000, 64, 3, 8, 10, 1, 8, 30000, 7, 36),      # eviction every tick
-    (5000, 256, 3, 8, 10, 2, 10, 50000, 11, 22),   # config-5 rules, smaller n
+    (300, 256, 3, 7, 0, 0, 10, 0, 1, 30),          # V > n - 1: everyone known
+    (2000, 64, 3, 7, 10, 1, 8, 30000, 7, 36),      # eviction every tick
+    (5000, 256, 3, 7, 10, 2, 10, 50000, 11, 22),   # config-5 rules, smaller n
     (3000, 32, 8, 2, 0, 1, 5, 20000, 3, 30),       # inbox overflow
     (1500, 100, 5, 4, 30, 2, 6, 100000, 99, 28),   # V not a power of 2
 ]
