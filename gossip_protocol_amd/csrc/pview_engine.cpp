@@ -78,7 +78,7 @@ namespace {
 
 int pview_validate(const gsp_pview_params *p) {
     GSP_REQUIRE(p, GSP_ERR_INVALID, "pview params NULL");
-    GSP_REQUIRE(p->n >= 2 && p->n <= (1 << 21), GSP_ERR_INVALID, "n=%d outside [2, 2^21]", p->n);
+    GSP_REQUIRE(p->n >= 2 && p->n < (1 << 21), GSP_ERR_INVALID, "n=%d outside [2, 2^21 - 1]", p->n);
     GSP_REQUIRE(p->view >= 1 && p->view <= gsp::kPvMaxView, GSP_ERR_INVALID, "view=%d outside [1, %d]",
                 p->view, gsp::kPvMaxView);
     GSP_REQUIRE(p->inbox >= 1 && p->inbox <= gsp::kPvMaxInbox, GSP_ERR_INVALID,

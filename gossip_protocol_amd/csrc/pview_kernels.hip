@@ -1,19 +1,24 @@
 // gossip_protocol_amd/csrc/pview_kernels.hip -- PARTIAL-VIEW tick kernel for gfx950.
 //
-// One 256-lane workgroup per receiver row; the row's work lives in LDS (~41 KB):
+// One 256-lane workgroup per receiver row; the row's work lives in ~25 KB of LDS (6 rows per
+// CU in flight):
 //   1. receipt order: its <= K smallest senders (canonical order; the rest = inbox overflow);
-//   2. keys: its own view and the K sender views, each a sorted block of 256 slots, as
-//      64-bit keys (id << 24 | source << 16 | hb << 5 | ts5); source 0 = own view, j = the
-//      payload of message j, so equal ids sort in message order;
-//   3. union: a tree of merge-path merges (one co-rank binary search per lane per level,
-//      then a short sequential merge): 256 -> 512 -> 1024 -> 2048 keys;
+//   2. keys: its own view and the k sender views, each a sorted block of 256 slots, as 32-bit
+//      keys id << 11 | source << 8 | slot (source 0 = own view, j = the payload of message j;
+//      the 16-bit value hb << 5 | ts5 stays behind in vals[source][slot]), so equal ids sort
+//      in message order;
+//   3. union: a tree of merge-path merges (one co-rank binary search per lane per level, then
+//      a register merge of the lane's kBlocks outputs): 256 -> 512 -> 1024 -> 2048 keys, with
+//      the lanes past the (k + 1) * 256 real keys idle;
 //   4. fold: the lane holding the first key of an id folds MP1Node::recvCallBack's rules over
 //      that id's run (own entry, sender event j, payload entry j, ...; MP1Node.cpp:234-301)
-//      and runs the TREMOVE test (MP1Node.cpp:339-348); senders found in no list become new
-//      (1, t) entries ("orphans");
-//   5. survivors compacted in id order, orphans merged in; eviction to V by (age, -hb, id)
-//      with an age histogram, an hb histogram of the boundary age and an id-order tie prefix;
-//   6. the new sorted view is written back (2 KB); Philox rank-select picks the peers.
+//      and runs the TREMOVE test (MP1Node.cpp:339-348).  A sender found in no list becomes a
+//      new (1, t) entry ("orphan"), adopted by the lane whose key range brackets its id;
+//   5. survivors compacted in id order (one block scan); eviction to V by (age, -hb, id) with
+//      an age histogram, an hb histogram of the boundary age and an id-order tie prefix, all
+//      resolved by a single packed block scan;
+//   6. the new sorted view is written back (2 KB, coalesced); Philox rank-select picks the
+//      peers (draws precomputed by lanes 0..F-1, drop draws in parallel).
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include "philox.hpp"
 #include "pview_kernels.hpp"
@@ -22,9 +27,11 @@ namespace gsp {
 namespace {
 
 constexpr int kSlots = kPvMaxView;                    // slots per source block
-constexpr int kMaxKeys = kSlots * (kPvMaxInbox + 1);  // 2048 with K = 7
-constexpr int kPerLane = kMaxKeys / kPvBlock;          // 8
-constexpr uint64_t kKeyMax = ~0ull;
+constexpr int kMaxBlocks = kPvMaxInbox + 1;           // own view + K sender views
+constexpr int kMaxKeys = kSlots * kMaxBlocks;         // 2048
+constexpr int kUCap = kMaxKeys + 8;                   // survivors + orphans
+constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: above every node id
+static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
 
 __device__ inline uint64_t pv_event_mix(uint32_t kind, uint32_t t, uint32_t r, uint32_t x) {
     uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) |
@@ -42,13 +49,16 @@ __device__ inline uint32_t pv_merge(uint32_t e, uint32_t v, uint32_t t5, uint32_
     return e ? upd : add;
 }
 
-__device__ inline int32_t key_id(uint64_t k) { return int32_t(k >> 24); }
-__device__ inline uint32_t key_src(uint64_t k) { return uint32_t(k >> 16) & 0xFFu; }
-__device__ inline uint32_t key_val(uint64_t k) { return uint32_t(k) & 0xFFFFu; }
-__device__ inline int32_t ent_id(uint64_t e) { return int32_t(e >> 32); }
-__device__ inline uint32_t ent_val(uint64_t e) { return uint32_t(e) & 0xFFFFu; }
+__device__ inline uint32_t key_id(uint32_t k) { return k >> 11; }
+__device__ inline uint32_t key_src(uint32_t k) { return (k >> 8) & 7u; }
+__device__ inline uint32_t key_slot(uint32_t k) { return k & 255u; }
 
-__device__ inline uint64_t wave_sum(uint64_t v) {
+__device__ inline uint32_t wave_sum32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ inline uint64_t wave_sum64(uint64_t v) {
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
@@ -77,54 +87,454 @@ __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_w
     return incl - v + before;
 }
 
-// number of elements of the ascending array a[0, n) that are < x (by id field)
-__device__ inline int32_t count_ids_below(const uint64_t *a, int32_t n, int32_t x) {
-    int32_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (ent_id(a[mid]) < x) lo = mid + 1; else hi = mid;
+template <int N>
+__device__ inline void lds_store(uint32_t *p, const uint32_t (&v)[N]) {
+    if constexpr (N == 1) {
+        p[0] = v[0];
+    } else if constexpr (N == 2) {
+        *reinterpret_cast<uint2 *>(p) = make_uint2(v[0], v[1]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i += 4)
+            *reinterpret_cast<uint4 *>(p + i) = make_uint4(v[i], v[i + 1], v[i + 2], v[i + 3]);
     }
-    return lo;
 }
 
-struct PvShared {
-    uint64_t keys[2][kMaxKeys];          // ping-pong buffers (32 KB)
-    uint32_t hist[2048];                 // eviction histograms (8 KB)
-    int32_t src[kPvMaxInbox], slot[kPvMaxInbox];
-    int32_t orphan[kPvMaxInbox];         // sender id if it is in no list, else -1
+template <int N>
+__device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
+    if constexpr (N == 1) {
+        v[0] = p[0];
+    } else if constexpr (N == 2) {
+        const uint2 x = *reinterpret_cast<const uint2 *>(p);
+        v[0] = x.x; v[1] = x.y;
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; i += 4) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(p + i);
+            v[i] = x.x; v[i + 1] = x.y; v[i + 2] = x.z; v[i + 3] = x.w;
+        }
+    }
+}
+
+struct alignas(16) PvShared {
+    uint32_t keys[2][kUCap];             // merge ping-pong; then survivor ids (U), kept ids (W)
+    uint16_t vals[kMaxKeys];             // values by (source, slot); then hb histogram; then W vals
+    uint16_t uval[kUCap];                // survivor values
+    uint32_t age_hist[32];
+    uint32_t peer_u[16];                 // Philox peer draws of lanes 0..F-1
+    int32_t pick[16], chosen[16];
+    int32_t src[kPvMaxInbox], slot[kPvMaxInbox], lenp[kPvMaxInbox], found[kPvMaxInbox];
     int32_t misc[8];
     uint32_t wave_scan[4];
     unsigned long long red[4][4];
 };
 
+struct RowOut {
+    const uint32_t *ids;
+    const uint16_t *vals;
+    int32_t len;
+    uint32_t joins, removes, evicts;
+    uint64_t hsum;
+};
+
+// Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 4 or 8).
+template <int kBlocks>
+__device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t lr,
+                                             int32_t r, int32_t k, RowOut &ro) {
+    constexpr int Q = kBlocks;                           // keys per lane
+    constexpr int P = kBlocks * kSlots;
+    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t V = a.view;
+    const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
+    const int32_t Pe = (k + 1) * kSlots;                // keys that can be real
+
+    // ---- 2. keys: one sorted block of 256 slots per source -----------------------------------
+    // every row load is issued before any is consumed (one HBM round trip, not k + 1)
+    uint64_t ent[kBlocks];
+#pragma unroll
+    for (int m = 0; m < kBlocks; ++m) {
+        ent[m] = kPvEmpty;
+        if (m <= k && tid < V) {
+            const uint64_t *row;
+            if (m == 0) row = a.prev + int64_t(lr) * V;
+            else {
+                const int32_t sl = sh.slot[m - 1];
+                row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
+            }
+            ent[m] = __builtin_nontemporal_load(row + tid);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < kBlocks; ++m) {
+        const bool ok = ent[m] != kPvEmpty;
+        sh.keys[0][m * kSlots + tid] =
+            ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
+        sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
+        if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
+    }
+    __syncthreads();
+
+    // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
+    const int32_t beg = tid * Q;
+    int cur = 0;
+#pragma unroll
+    for (int s = kSlots; s < P; s <<= 1) {
+        if (beg < Pe) {
+            const uint32_t *X = sh.keys[cur];
+            uint32_t *Y = sh.keys[cur ^ 1];
+            const int32_t b = beg / (2 * s), o = beg - b * 2 * s;
+            const uint32_t *A = X + b * 2 * s, *B = A + s;
+            int32_t lo = o > s ? o - s : 0, hi = o < s ? o : s;
+            while (lo < hi) {                                  // co-rank of output o
+                const int32_t mid = (lo + hi) >> 1;
+                if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
+            }
+            int32_t i = lo, j = o - lo;
+            uint32_t va = i < s ? A[i] : kKeyMax, vb = j < s ? B[j] : kKeyMax;
+            uint32_t outk[Q];
+#pragma unroll
+            for (int e = 0; e < Q; ++e) {
+                const bool ta = va <= vb;                      // equal only for padding
+                outk[e] = ta ? va : vb;
+                i += ta ? 1 : 0;
+                j += ta ? 0 : 1;
+                const int32_t ii = ta ? i : j;
+                const uint32_t nv = ii < s ? (ta ? A : B)[ii] : kKeyMax;
+                va = ta ? nv : va;
+                vb = ta ? vb : nv;
+            }
+            lds_store<Q>(Y + beg, outk);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+    const uint32_t *C = sh.keys[cur];
+
+    // ---- 4. fold each id's run ------------------------------------------------------------
+    uint32_t ck[Q];
+    lds_load<Q>(C + beg, ck);
+    const uint32_t lo_id = tid > 0 ? key_id(C[beg - 1]) + 1u : 0u;  // this lane brackets ids
+    const uint32_t hi_id = tid < kPvBlock - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
+    uint32_t ssrc[kPvMaxInbox];
+#pragma unroll
+    for (int jj = 0; jj < kPvMaxInbox; ++jj) ssrc[jj] = jj < k ? uint32_t(sh.src[jj]) : kKeyMax;
+
+    uint32_t res[Q], rid[Q];
+    uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
+    uint64_t hsum = 0;
+#pragma unroll
+    for (int e = 0; e < Q; ++e) {
+        res[e] = 0;
+        rid[e] = 0;
+        const uint32_t kk0 = ck[e];
+        const uint32_t x = key_id(kk0);
+        const bool first = e == 0 ? x >= lo_id : x != key_id(ck[e - 1]);
+        if (kk0 == kKeyMax || !first) continue;
+        int32_t jsend = 0;
+#pragma unroll
+        for (int jj = 0; jj < kPvMaxInbox; ++jj) jsend = ssrc[jj] == x ? jj + 1 : jsend;
+        if (jsend) found_mask |= 1u << (jsend - 1);
+        if (x == uint32_t(r)) continue;                       // never list yourself
+        int32_t pos = beg + e;
+        uint32_t nk = kk0, v = 0, e0 = 0;
+        if (key_src(nk) == 0) {
+            e0 = v = sh.vals[key_slot(nk)];
+            ++pos;
+            nk = pos < Pe ? C[pos] : kKeyMax;
+        }
+        for (int32_t jj = 1; jj <= k; ++jj) {
+            if (jj == jsend) v = (((v >> 5) + 1u) << 5) | t5;              // MP1Node.cpp:237-243
+            if (key_id(nk) == x && key_src(nk) == uint32_t(jj)) {
+                v = pv_merge(v, sh.vals[jj * kSlots + key_slot(nk)], t5, tr);  // MP1Node.cpp:247-301
+                ++pos;
+                nk = pos < Pe ? C[pos] : kKeyMax;
+            }
+        }
+        if (!v) continue;
+        if (!e0) { joins++; hsum += pv_event_mix(1, t, uint32_t(r), x); }
+        if (((t5 - v) & 31u) >= tr) {                          // TREMOVE scan
+            removes++;
+            hsum += pv_event_mix(2, t, uint32_t(r), x);
+            continue;
+        }
+        res[e] = v;
+        rid[e] = x;
+        nloc++;
+    }
+    // candidate orphans: senders whose id falls in this lane's bracket
+    uint32_t adopt = 0;
+    int32_t ains[kPvMaxInbox];
+#pragma unroll
+    for (int jj = 0; jj < kPvMaxInbox; ++jj) {
+        ains[jj] = 0;
+        const uint32_t x = ssrc[jj];
+        if (jj < k && x >= lo_id && x <= hi_id && beg <= Pe) {
+            int32_t c = 0;
+#pragma unroll
+            for (int e = 0; e < Q; ++e) c += key_id(ck[e]) < x ? 1 : 0;
+            ains[jj] = c;
+            adopt |= 1u << jj;
+        }
+    }
+    if (found_mask) {
+#pragma unroll
+        for (int jj = 0; jj < kPvMaxInbox; ++jj)
+            if ((found_mask >> jj) & 1u) sh.found[jj] = 1;
+    }
+    __syncthreads();
+    if (adopt) {
+#pragma unroll
+        for (int jj = 0; jj < kPvMaxInbox; ++jj) {
+            if (!((adopt >> jj) & 1u)) continue;
+            if (sh.found[jj]) { adopt &= ~(1u << jj); continue; }
+            nloc++;
+            joins++;
+            hsum += pv_event_mix(1, t, uint32_t(r), ssrc[jj]);
+        }
+    }
+
+    // ---- 5a. survivors (and adopted orphans), compacted in id order -------------------------
+    uint32_t total = 0;
+    const uint32_t base = block_scan(nloc, &total, sh.wave_scan);
+    uint32_t *Uid = sh.keys[cur ^ 1];
+    uint16_t *Uval = sh.uval;
+    const bool evict = int32_t(total) > V;
+    {
+        uint32_t w = base;
+        if (!adopt) {
+#pragma unroll
+            for (int e = 0; e < Q; ++e)
+                if (res[e]) {
+                    Uid[w] = rid[e];
+                    Uval[w] = uint16_t(res[e]);
+                    if (evict) atomicAdd(&sh.age_hist[(t5 - res[e]) & 31u], 1u);
+                    w++;
+                }
+        } else {
+            const uint32_t fresh = (1u << 5) | t5;             // an orphan: (hb 1, ts t)
+#pragma unroll
+            for (int e = 0; e <= Q; ++e) {
+#pragma unroll
+                for (int jj = 0; jj < kPvMaxInbox; ++jj)
+                    if (((adopt >> jj) & 1u) && ains[jj] == e) {
+                        Uid[w] = ssrc[jj];
+                        Uval[w] = uint16_t(fresh);
+                        if (evict) atomicAdd(&sh.age_hist[0], 1u);
+                        w++;
+                    }
+                if (e < Q && res[e]) {
+                    Uid[w] = rid[e];
+                    Uval[w] = uint16_t(res[e]);
+                    if (evict) atomicAdd(&sh.age_hist[(t5 - res[e]) & 31u], 1u);
+                    w++;
+                }
+            }
+        }
+    }
+    ro.ids = Uid;
+    ro.vals = Uval;
+    ro.len = int32_t(total);
+
+    // ---- 5b. eviction to V by (age, -hb, id) ------------------------------------------------
+    if (evict) {
+        uint32_t *hist = reinterpret_cast<uint32_t *>(sh.vals);   // 2048 hb bins, u16 pairs
+        for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
+        __syncthreads();
+        if (wave == 0) {                                   // boundary age: first cum >= V
+            const uint32_t hv = lane < 32 ? sh.age_hist[lane] : 0u;
+            uint32_t incl = hv;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t u = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += u;
+            }
+            const unsigned long long hit = __ballot(lane < 32 && incl >= uint32_t(V));
+            const int32_t ab = __builtin_ffsll(hit) - 1;
+            const uint32_t before = __shfl(incl - hv, ab, 64);
+            const uint32_t at = __shfl(hv, ab, 64);
+            if (lane == 0) {
+                sh.misc[0] = ab;
+                sh.misc[1] = V - int32_t(before);          // kept at the boundary age
+                sh.misc[2] = int32_t(at);
+            }
+        }
+        __syncthreads();
+        const uint32_t astar = uint32_t(sh.misc[0]);
+        const int32_t need = sh.misc[1];
+        const bool tie = sh.misc[2] > need;
+        uint32_t hstar = 0;
+        int32_t need2 = 0;
+        if (tie) {                                         // boundary hb among age == astar
+            for (uint32_t i = base; i < base + nloc; ++i) {
+                const uint32_t v = Uval[i];
+                if (((t5 - v) & 31u) == astar)
+                    atomicAdd(&hist[(v >> 5) >> 1], 1u << (((v >> 5) & 1u) * 16u));
+            }
+            __syncthreads();
+            // lane t owns hb bins 2047 - 8t - 7 .. 2047 - 8t (descending order of lanes)
+            const uint16_t *h16 = sh.vals;
+            uint32_t loc = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b) loc += h16[2047 - 8 * tid - b];
+            uint32_t tot = 0;
+            const uint32_t ex = block_scan(loc, &tot, sh.wave_scan);
+            if (ex < uint32_t(need) && uint32_t(need) <= ex + loc) {
+                uint32_t cum = ex;
+                for (int b = 0; b < 8; ++b) {
+                    const int32_t h = 2047 - 8 * tid - b;
+                    const uint32_t c = h16[h];
+                    if (cum + c >= uint32_t(need)) {
+                        sh.misc[3] = h;
+                        sh.misc[4] = need - int32_t(cum);  // kept among (astar, h) ties
+                        break;
+                    }
+                    cum += c;
+                }
+            }
+            __syncthreads();
+            hstar = uint32_t(sh.misc[3]);
+            need2 = sh.misc[4];
+        }
+        // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
+        uint32_t nt = 0, nk = 0;
+        for (uint32_t i = base; i < base + nloc; ++i) {
+            const uint32_t v = Uval[i], age = (t5 - v) & 31u, hb = v >> 5;
+            const bool is_tie = tie && age == astar && hb == hstar;
+            nt += is_tie ? 1u : 0u;
+            nk += (!is_tie && (age < astar || (age == astar && (!tie || hb > hstar)))) ? 1u : 0u;
+        }
+        uint32_t sums = 0;
+        const uint32_t ex = block_scan(nt | (nk << 16), &sums, sh.wave_scan);
+        uint32_t tie_before = ex & 0xFFFFu;
+        const uint32_t ties_kept_before = tie_before < uint32_t(need2) ? tie_before : uint32_t(need2);
+        uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
+        uint32_t *Wid = sh.keys[cur];                       // C is dead
+        uint16_t *Wval = sh.vals;                           // the histogram is dead
+        for (uint32_t i = base; i < base + nloc; ++i) {
+            const uint32_t v = Uval[i], age = (t5 - v) & 31u, hb = v >> 5;
+            bool keep = age < astar || (age == astar && (!tie || hb > hstar));
+            if (tie && age == astar && hb == hstar) keep = int32_t(tie_before++) < need2;
+            if (keep) {
+                Wid[w] = Uid[i];
+                Wval[w] = uint16_t(v);
+                w++;
+            } else {
+                evicts++;
+                hsum += pv_event_mix(3, t, uint32_t(r), Uid[i]);
+            }
+        }
+        ro.ids = Wid;
+        ro.vals = Wval;
+        ro.len = V;
+    }
+    ro.joins = joins;
+    ro.removes = removes;
+    ro.evicts = evicts;
+    ro.hsum = hsum;
+    __syncthreads();
+}
+
+// ---- 6. write the view, heartbeat, digest, sends ------------------------------------------
+__device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, int32_t lr,
+                                          int32_t r, int32_t k, int32_t k_all, bool init,
+                                          const RowOut &ro) {
+    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t V = a.view, F = a.fanout, len = ro.len;
+    const uint32_t t = uint32_t(a.tick);
+    uint64_t *out = a.cur + int64_t(lr) * V;
+    for (int32_t i = tid; i < V; i += kPvBlock)
+        __builtin_nontemporal_store(
+            i < len ? (uint64_t(ro.ids[i]) << 32) | uint64_t(ro.vals[i]) : kPvEmpty, out + i);
+
+    unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
+    if (!init) {
+        const uint32_t j = wave_sum32(ro.joins), rm = wave_sum32(ro.removes), ev = wave_sum32(ro.evicts);
+        const uint64_t h = wave_sum64(ro.hsum);
+        if (lane == 0) { sh.red[wave][0] = j; sh.red[wave][1] = rm; sh.red[wave][2] = ev; sh.red[wave][3] = h; }
+        __syncthreads();
+    }
+    if (wave != 0) return;
+    // peers: min(F, len) distinct members by Philox rank-select over the id order
+    const int32_t keff = F < len ? F : len;
+    if (lane == 0) {
+        int32_t nch = 0;
+        for (int32_t kk = 0; kk < keff; ++kk) {
+            int32_t rk = int32_t(sh.peer_u[kk] % uint32_t(len - kk));
+            int32_t pos = 0;
+            while (pos < nch && rk >= sh.chosen[pos]) { rk++; pos++; }
+            for (int32_t q2 = nch; q2 > pos; --q2) sh.chosen[q2] = sh.chosen[q2 - 1];
+            sh.chosen[pos] = rk;
+            nch++;
+            sh.pick[kk] = int32_t(ro.ids[rk]);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    bool drop = false;
+    if (lane < F) {
+        int32_t dst = -1;
+        if (lane < keff) {
+            dst = sh.pick[lane];
+            const uint32_t dr = draw_u31(kDomainSend, a.seed, t, uint32_t(r), uint32_t(dst), 3u);
+            if (int32_t(dr % 100u) < a.drop_pct) { drop = true; dst = -1; }
+        }
+        a.out_dst[int64_t(lr) * F + lane] = dst;
+        if (dst >= 0) atomicAdd(&a.deg[dst], 1);
+    }
+    const uint32_t dropped = uint32_t(__popcll(__ballot(drop)));
+    if (lane == 0) {
+        a.len_cur[r] = len;
+        if (keff) {
+            atomicAdd(&dig[kPvSent], (unsigned long long)keff);
+            if (dropped) atomicAdd(&dig[kPvDropped], (unsigned long long)dropped);
+        }
+        if (!init) {
+            a.own_hb[lr] += 1;
+            unsigned long long merges = 0;
+            for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(sh.lenp[j]);
+            atomicAdd(&dig[kPvRounds], 1ull);
+            atomicAdd(&dig[kPvMerges], merges);
+            atomicAdd(&dig[kPvDelivered], (unsigned long long)k);
+            if (k_all > k) atomicAdd(&dig[kPvOverflow], (unsigned long long)(k_all - k));
+            const unsigned long long j = sh.red[0][0] + sh.red[1][0] + sh.red[2][0] + sh.red[3][0];
+            const unsigned long long rm = sh.red[0][1] + sh.red[1][1] + sh.red[2][1] + sh.red[3][1];
+            const unsigned long long ev = sh.red[0][2] + sh.red[1][2] + sh.red[2][2] + sh.red[3][2];
+            if (j) atomicAdd(&dig[kPvJoins], j);
+            if (rm) atomicAdd(&dig[kPvRemoves], rm);
+            if (ev) atomicAdd(&dig[kPvEvicts], ev);
+            atomicAdd(&dig[kPvHash], sh.red[0][3] + sh.red[1][3] + sh.red[2][3] + sh.red[3][3]);
+        }
+    }
+}
+
 template <bool kInit>
 __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared sh;
-    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t tid = threadIdx.x;
     const int32_t lr = blockIdx.x;
     const int32_t r = a.row0 + lr;
-    const int32_t t = a.tick, F = a.fanout, V = a.view;
-    const uint32_t t5 = uint32_t(t) & 31u, tr = uint32_t(a.tremove);
+    const int32_t F = a.fanout, V = a.view;
 
-    if (t > a.fail_tick[r]) {          // crashed: no recv, no ops, no send
+    if (a.tick > a.fail_tick[r]) {          // crashed: no recv, no ops, no send
         if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
         return;
     }
+    if (tid < F)
+        sh.peer_u[tid] = draw_u31(kDomainPeer, a.seed, uint32_t(a.tick), uint32_t(r), uint32_t(tid), 0u);
+    if (tid < 32) sh.age_hist[tid] = 0;
+    if (tid < kPvMaxInbox) sh.found[tid] = 0;
 
-    // the new view ends up in view_buf as (id << 32 | val), id order
-    const uint64_t *view_buf = sh.keys[0];
-    int32_t new_len = 0;
-    uint64_t joins = 0, removes = 0, evicts = 0, hsum = 0;
+    RowOut ro{};
     int32_t k = 0, k_all = 0;
-
     if (kInit) {
         // pre-joined bounded view: {(r + 1 + j * (n / V)) mod n}, or everyone if n - 1 <= V
         const int32_t n = a.n;
-        const uint64_t h = uint64_t(a.h0) << 5;
+        uint32_t *ids = sh.keys[0];
         if (n - 1 <= V) {
             for (int32_t x = tid; x < n; x += kPvBlock)
-                if (x != r) sh.keys[0][x < r ? x : x - 1] = (uint64_t(x) << 32) | h;
-            new_len = n - 1;
+                if (x != r) ids[x < r ? x : x - 1] = uint32_t(x);
+            ro.len = n - 1;
         } else {
             const int64_t stride = n / V;
             const int64_t first_wrap = (int64_t(n) - r - 1 + stride - 1) / stride;
@@ -133,10 +543,13 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
                 int64_t x = int64_t(r) + 1 + int64_t(j) * stride;
                 int32_t p;
                 if (x >= n) { x -= n; p = j - J; } else { p = j + (V - J); }
-                sh.keys[0][p] = (uint64_t(x) << 32) | h;
+                ids[p] = uint32_t(x);
             }
-            new_len = V;
+            ro.len = V;
         }
+        for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.uval[i] = uint16_t(a.h0 << 5);
+        ro.ids = ids;
+        ro.vals = sh.uval;
         __syncthreads();
     } else {
         // ---- 1. receipt order --------------------------------------------------------------
@@ -158,314 +571,27 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
         for (int32_t i = tid; i < k_all; i += kPvBlock) {
             int32_t rank = 0;
             for (int32_t j = 0; j < k_all; ++j) rank += raw[j] < raw[i];
-            if (rank < k) { sh.src[rank] = raw[i]; sh.slot[rank] = raw_slot[i]; }
+            if (rank < k) {
+                sh.src[rank] = raw[i];
+                sh.slot[rank] = raw_slot[i];
+                sh.lenp[rank] = a.len_prev[raw[i]];            // sender view sizes (merges)
+            }
         }
         __syncthreads();
-
-        // ---- 2. keys: one sorted block of 256 slots per source ------------------------------
-        int32_t blocks = 1;
-        while (blocks < k + 1) blocks <<= 1;
-        for (int32_t m = 0; m < blocks; ++m) {
-            uint64_t key = kKeyMax;
-            if (m <= k && tid < V) {
-                const uint64_t *row;
-                if (m == 0) row = a.prev + int64_t(lr) * V;
-                else {
-                    const int32_t sl = sh.slot[m - 1];
-                    row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
-                }
-                const uint64_t ent = row[tid];
-                if (ent != kPvEmpty)
-                    key = ((ent >> 32) << 24) | (uint64_t(m) << 16) | (ent & 0xFFFFu);
-            }
-            sh.keys[0][m * kSlots + tid] = key;
-        }
-        __syncthreads();
-
-        // ---- 3. merge-path tree: sorted union of every source, ties in message order --------
-        const int32_t P = blocks * kSlots;
-        const int32_t q = P / kPvBlock;                       // keys per lane
-        int32_t cur = 0;
-        for (int32_t s = kSlots; s < P; s <<= 1) {
-            const uint64_t *X = sh.keys[cur];
-            uint64_t *Y = sh.keys[cur ^ 1];
-            const int32_t beg = tid * q;
-            const int32_t b = beg / (2 * s);
-            const int32_t o = beg - b * 2 * s;
-            const uint64_t *A = X + b * 2 * s, *B = A + s;
-            int32_t lo = o > s ? o - s : 0, hi = o < s ? o : s;
-            while (lo < hi) {                                  // co-rank of output o
-                const int32_t mid = (lo + hi) >> 1;
-                if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
-            }
-            int32_t i = lo, j = o - lo;
-            uint64_t *dst = Y + b * 2 * s + o;
-            for (int32_t e = 0; e < q; ++e) {
-                const uint64_t va = i < s ? A[i] : kKeyMax;
-                const uint64_t vb = j < s ? B[j] : kKeyMax;
-                const bool ta = j >= s || (i < s && va < vb);
-                dst[e] = ta ? va : vb;
-                i += ta ? 1 : 0;
-                j += ta ? 0 : 1;
-            }
-            __syncthreads();
-            cur ^= 1;
-        }
-        const uint64_t *C = sh.keys[cur];
-
-        // ---- 4. fold each id's run ----------------------------------------------------------
-        const int32_t beg = tid * q;
-        uint32_t res[kPerLane];
-        int32_t rid[kPerLane];
-        uint32_t nloc = 0;
-#pragma unroll
-        for (int32_t e = 0; e < kPerLane; ++e) {
-            res[e] = 0;
-            rid[e] = 0;
-            if (e >= q) continue;
-            const int32_t p = beg + e;
-            const uint64_t key = C[p];
-            if (key == kKeyMax) continue;
-            const int32_t x = key_id(key);
-            if (p > 0 && key_id(C[p - 1]) == x) continue;      // not the first key of its run
-            if (x == r) continue;                              // never list yourself
-            int32_t pos = p;
-            uint32_t e0 = 0;
-            if (key_src(key) == 0) { e0 = key_val(key); pos++; }
-            uint32_t v = e0;
-            for (int32_t jj = 1; jj <= k; ++jj) {
-                if (sh.src[jj - 1] == x) v = (((v >> 5) + 1u) << 5) | t5;   // MP1Node.cpp:237-243
-                if (pos < P) {
-                    const uint64_t kk = C[pos];
-                    if (key_id(kk) == x && key_src(kk) == uint32_t(jj)) {
-                        v = pv_merge(v, key_val(kk), t5, tr);                 // MP1Node.cpp:247-301
-                        pos++;
-                    }
-                }
-            }
-            if (!v) continue;
-            if (!e0) { joins++; hsum += pv_event_mix(1, uint32_t(t), uint32_t(r), uint32_t(x)); }
-            if (((t5 - v) & 31u) >= tr) {                      // TREMOVE scan
-                removes++;
-                hsum += pv_event_mix(2, uint32_t(t), uint32_t(r), uint32_t(x));
-                continue;
-            }
-            res[e] = v;
-            rid[e] = x;
-            nloc++;
-        }
-        // senders that are in no list: their sender event is their only event -> (1, t)
-        if (tid < k) {
-            const int32_t x = sh.src[tid];
-            int32_t lo = 0, hi = P;
-            const uint64_t probe = uint64_t(uint32_t(x)) << 24;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi) >> 1;
-                if (C[mid] < probe) lo = mid + 1; else hi = mid;
-            }
-            const bool found = lo < P && C[lo] != kKeyMax && key_id(C[lo]) == x;
-            sh.orphan[tid] = found ? -1 : x;
-            if (!found) { joins++; hsum += pv_event_mix(1, uint32_t(t), uint32_t(r), uint32_t(x)); }
-        }
-        // ---- 5a. survivors, compacted in id order into the other buffer ---------------------
-        uint32_t n_surv = 0;
-        const uint32_t base = block_scan(nloc, &n_surv, sh.wave_scan);   // fences C reads
-        uint64_t *S = sh.keys[cur ^ 1];
-        {
-            uint32_t w = base;
-#pragma unroll
-            for (int32_t e = 0; e < kPerLane; ++e)
-                if (res[e]) S[w++] = (uint64_t(uint32_t(rid[e])) << 32) | res[e];
-        }
-        __syncthreads();
-        // ---- 5b. merge the (<= K, ascending) orphans in: into buffer `cur` (C is done) ------
-        int32_t n_orph = 0;
-        for (int32_t jj = 0; jj < k; ++jj) n_orph += sh.orphan[jj] >= 0 ? 1 : 0;
-        uint64_t *U = sh.keys[cur];
-        const int32_t total = int32_t(n_surv) + n_orph;
-        for (int32_t i = tid; i < int32_t(n_surv); i += kPvBlock) {
-            const uint64_t ent = S[i];
-            int32_t shift = 0;
-            for (int32_t jj = 0; jj < k; ++jj) {
-                const int32_t o = sh.orphan[jj];
-                shift += (o >= 0 && o < ent_id(ent)) ? 1 : 0;
-            }
-            U[i + shift] = ent;
-        }
-        if (tid < k && sh.orphan[tid] >= 0) {
-            const int32_t x = sh.orphan[tid];
-            int32_t below = 0;
-            for (int32_t jj = 0; jj < tid; ++jj) below += sh.orphan[jj] >= 0 ? 1 : 0;  // ascending
-            const int32_t pos = count_ids_below(S, int32_t(n_surv), x) + below;
-            U[pos] = (uint64_t(uint32_t(x)) << 32) | ((1u << 5) | t5);
-        }
-        __syncthreads();
-        view_buf = U;
-        new_len = total;
-
-        // ---- 5c. eviction to V by (age, -hb, id) --------------------------------------------
-        if (total > V) {
-            for (int32_t i = tid; i < 2048; i += kPvBlock) sh.hist[i] = 0;
-            __syncthreads();
-            for (int32_t i = tid; i < total; i += kPvBlock)
-                atomicAdd(&sh.hist[(t5 - ent_val(U[i])) & 31u], 1u);
-            __syncthreads();
-            if (wave == 0) {                                   // boundary age: first cum >= V
-                const uint32_t hv = lane < 32 ? sh.hist[lane] : 0u;
-                uint32_t incl = hv;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t u = __shfl_up(incl, d, 64);
-                    if (lane >= d) incl += u;
-                }
-                const unsigned long long hit = __ballot(lane < 32 && incl >= uint32_t(V));
-                const int32_t ab = __builtin_ffsll(hit) - 1;
-                const uint32_t before = __shfl(incl - hv, ab, 64);
-                if (lane == 0) {
-                    sh.misc[0] = ab;
-                    sh.misc[1] = V - int32_t(before);          // kept at the boundary age
-                    sh.misc[2] = int32_t(sh.hist[ab]);
-                }
-            }
-            __syncthreads();
-            const uint32_t astar = uint32_t(sh.misc[0]);
-            const int32_t need = sh.misc[1];
-            const bool tie = sh.misc[2] > need;
-            if (tie) {                                         // boundary hb among age == astar
-                for (int32_t i = tid; i < 2048; i += kPvBlock) sh.hist[i] = 0;
-                __syncthreads();
-                for (int32_t i = tid; i < total; i += kPvBlock) {
-                    const uint32_t v = ent_val(U[i]);
-                    if (((t5 - v) & 31u) == astar) atomicAdd(&sh.hist[v >> 5], 1u);
-                }
-                __syncthreads();
-                // lane t owns hb bins 2047 - 8t - 7 .. 2047 - 8t (descending order of lanes)
-                uint32_t loc = 0;
-#pragma unroll
-                for (int b = 0; b < 8; ++b) loc += sh.hist[2047 - 8 * tid - b];
-                uint32_t tot = 0;
-                const uint32_t ex = block_scan(loc, &tot, sh.wave_scan);
-                if (ex < uint32_t(need) && uint32_t(need) <= ex + loc) {
-                    uint32_t cum = ex;
-                    for (int b = 0; b < 8; ++b) {
-                        const int32_t h = 2047 - 8 * tid - b;
-                        if (cum + sh.hist[h] >= uint32_t(need)) {
-                            sh.misc[3] = h;
-                            sh.misc[4] = need - int32_t(cum);  // kept among (astar, h) ties
-                            break;
-                        }
-                        cum += sh.hist[h];
-                    }
-                }
-                __syncthreads();
-            }
-            const uint32_t hstar = tie ? uint32_t(sh.misc[3]) : 0u;
-            const int32_t need2 = tie ? sh.misc[4] : 0;
-            // contiguous ranges per lane keep the id order for the tie prefix and compaction
-            const int32_t per = (total + kPvBlock - 1) / kPvBlock;
-            const int32_t b0 = tid * per;
-            uint32_t nt = 0;
-            for (int32_t e = 0; e < per; ++e) {
-                const int32_t i = b0 + e;
-                if (i >= total) break;
-                const uint32_t v = ent_val(U[i]);
-                nt += (tie && ((t5 - v) & 31u) == astar && (v >> 5) == hstar) ? 1u : 0u;
-            }
-            uint32_t ntot = 0;
-            uint32_t tie_before = block_scan(nt, &ntot, sh.wave_scan);
-            uint32_t keep_cnt = 0;
-            uint32_t keep_mask = 0;                            // per <= 9 entries of this lane
-            for (int32_t e = 0; e < per; ++e) {
-                const int32_t i = b0 + e;
-                if (i >= total) break;
-                const uint64_t ent = U[i];
-                const uint32_t v = ent_val(ent), age = (t5 - v) & 31u, hb = v >> 5;
-                bool keep = age < astar || (age == astar && (!tie || hb > hstar));
-                if (tie && age == astar && hb == hstar) {
-                    keep = int32_t(tie_before) < need2;
-                    tie_before++;
-                }
-                if (keep) { keep_mask |= 1u << e; keep_cnt++; }
-                else {
-                    evicts++;
-                    hsum += pv_event_mix(3, uint32_t(t), uint32_t(r), uint32_t(ent_id(ent)));
-                }
-            }
-            uint32_t kept = 0;
-            const uint32_t kbase = block_scan(keep_cnt, &kept, sh.wave_scan);
-            uint64_t *W = sh.keys[cur ^ 1];
-            uint32_t w = kbase;
-            for (int32_t e = 0; e < per; ++e) {
-                const int32_t i = b0 + e;
-                if (i >= total) break;
-                if (keep_mask & (1u << e)) W[w++] = U[i];
-            }
-            __syncthreads();
-            view_buf = W;
-            new_len = int32_t(kept);
-        }
+        if (k == 0) pv_merge_row<1>(a, sh, lr, r, k, ro);
+        else if (k == 1) pv_merge_row<2>(a, sh, lr, r, k, ro);
+        else if (k <= 3) pv_merge_row<4>(a, sh, lr, r, k, ro);
+        else pv_merge_row<8>(a, sh, lr, r, k, ro);
     }
-
-    // ---- 6. write the new view; heartbeat; send ------------------------------------------
-    uint64_t *out = a.cur + int64_t(lr) * V;
-    for (int32_t i = tid; i < V; i += kPvBlock) out[i] = i < new_len ? view_buf[i] : kPvEmpty;
-
-    const uint64_t r0 = wave_sum(joins), r1 = wave_sum(removes), r2 = wave_sum(evicts), r3 = wave_sum(hsum);
-    if (lane == 0) { sh.red[wave][0] = r0; sh.red[wave][1] = r1; sh.red[wave][2] = r2; sh.red[wave][3] = r3; }
-    __syncthreads();
-    unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
-    if (tid == 0) {
-        a.len_cur[r] = new_len;
-        if (!kInit) {
-            a.own_hb[lr] += 1;
-            unsigned long long merges = 0;
-            for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(a.len_prev[sh.src[j]]);
-            atomicAdd(&dig[kPvRounds], 1ull);
-            atomicAdd(&dig[kPvMerges], merges);
-            atomicAdd(&dig[kPvDelivered], (unsigned long long)k);
-            if (k_all > k) atomicAdd(&dig[kPvOverflow], (unsigned long long)(k_all - k));
-            atomicAdd(&dig[kPvJoins], sh.red[0][0] + sh.red[1][0] + sh.red[2][0] + sh.red[3][0]);
-            atomicAdd(&dig[kPvRemoves], sh.red[0][1] + sh.red[1][1] + sh.red[2][1] + sh.red[3][1]);
-            atomicAdd(&dig[kPvEvicts], sh.red[0][2] + sh.red[1][2] + sh.red[2][2] + sh.red[3][2]);
-            atomicAdd(&dig[kPvHash], sh.red[0][3] + sh.red[1][3] + sh.red[2][3] + sh.red[3][3]);
-        }
-        // peers: min(F, len) distinct members by Philox rank-select over the id order
-        const int32_t keff = F < new_len ? F : new_len;
-        int32_t chosen[16];
-        int32_t nch = 0;
-        unsigned long long sent = 0, dropped = 0;
-        for (int32_t kk = 0; kk < F; ++kk) {
-            int32_t dst = -1;
-            if (kk < keff) {
-                const uint32_t u = draw_u31(kDomainPeer, a.seed, uint32_t(t), uint32_t(r),
-                                            uint32_t(kk), 0u);
-                int32_t rk = int32_t(u % uint32_t(new_len - kk));
-                int32_t pos = 0;
-                while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
-                for (int32_t q2 = nch; q2 > pos; --q2) chosen[q2] = chosen[q2 - 1];
-                chosen[pos] = rk;
-                nch++;
-                dst = ent_id(view_buf[rk]);
-                sent++;
-                const uint32_t dr = draw_u31(kDomainSend, a.seed, uint32_t(t), uint32_t(r),
-                                             uint32_t(dst), 3u);
-                if (int32_t(dr % 100u) < a.drop_pct) { dropped++; dst = -1; }
-            }
-            a.out_dst[int64_t(lr) * F + kk] = dst;
-            if (dst >= 0) atomicAdd(&a.deg[dst], 1);
-        }
-        if (sent) {
-            atomicAdd(&dig[kPvSent], sent);
-            atomicAdd(&dig[kPvDropped], dropped);
-        }
-    }
+    (void)V;
+    pv_finish(a, sh, lr, r, k, k_all, kInit, ro);
 }
 
 }  // namespace
 
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st) {
     if (a.view < 1 || a.view > kPvMaxView || a.inbox < 1 || a.inbox > kPvMaxInbox ||
-        a.fanout < 1 || a.fanout > 16)
+        a.fanout < 1 || a.fanout > 16 || a.n >= (1 << 21))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(pview_tick_kernel<true>, dim3(a.rows), dim3(kPvBlock), 0, st, a);
     return hipGetLastError();
@@ -473,7 +599,7 @@ hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st) {
 
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     if (a.view < 1 || a.view > kPvMaxView || a.inbox < 1 || a.inbox > kPvMaxInbox ||
-        a.fanout < 1 || a.fanout > 16)
+        a.fanout < 1 || a.fanout > 16 || a.n >= (1 << 21))
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(pview_tick_kernel<false>, dim3(a.rows), dim3(kPvBlock), 0, st, a);
     return hipGetLastError();

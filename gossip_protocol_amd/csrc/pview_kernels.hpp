@@ -17,7 +17,7 @@ constexpr int kPvMaxInbox = 7;        // K <= 7 messages merged per receiver per
 constexpr uint64_t kPvEmpty = ~0ull;
 enum : int { kPvRounds = 0, kPvMerges, kPvSent, kPvDropped, kPvDelivered, kPvOverflow,
              kPvJoins, kPvRemoves, kPvEvicts, kPvHash, kPvFields };
-constexpr int kPvDigSlots = 64;
+constexpr int kPvDigSlots = 256;   // spread the per-row digest atomics
 
 struct PviewTickArgs {
     const uint64_t *prev;        // view table of tick t-1 (this shard's rows)

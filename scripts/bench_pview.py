@@ -75,7 +75,7 @@ def main():
         "ms_per_step": el * 1e3 / args.steps, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "u64 entries (id:32 | hb:11 | ts5)",
         "data": "synthetic (ring-initialised bounded views, Philox peers/drops/failures)",
-        "config": {"workload": "config5: %d nodes, partial view V=256, fanout 3, inbox 8, "
+        "config": {"workload": "config5: %d nodes, partial view V=256, fanout 3, inbox 7, "
                                "10%% drop, 5%% contiguous crash at t=10" % args.nodes},
         "merges_per_s": merges / el,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
