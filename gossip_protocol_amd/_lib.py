@@ -55,7 +55,8 @@ class GspScaleDigest(ctypes.Structure):
 
 class GspScalePerf(ctypes.Structure):
     _fields_ = [("ticks", c_int64), ("merge_launches", c_int64), ("merge_ms", ctypes.c_double),
-                ("csr_ms", ctypes.c_double), ("bytes_per_tick", ctypes.c_double)]
+                ("csr_ms", ctypes.c_double), ("bytes_per_tick", ctypes.c_double),
+                ("xgmi_bytes", ctypes.c_double)]
 
 
 class GspPviewParams(ctypes.Structure):
@@ -123,6 +124,12 @@ SIGNATURES = {
     "gsp_scale_layout": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), P(c_int64)]),
     "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
     "gsp_pview_create": (ctypes.c_int, [P(GspPviewParams), ctypes.c_int, P(ctypes.c_void_p)]),
+    "gsp_pview_create_rank": (ctypes.c_int, [P(GspPviewParams), ctypes.c_int, c_int32, c_int32,
+                                             ctypes.c_void_p, P(ctypes.c_void_p)]),
+    "gsp_pview_create_group": (ctypes.c_int, [P(GspPviewParams), ctypes.c_int, c_int32,
+                                              P(ctypes.c_void_p)]),
+    "gsp_pview_layout": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), P(c_int32),
+                                        P(c_int32)]),
     "gsp_pview_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "gsp_pview_step": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
     "gsp_pview_sync": (ctypes.c_int, [ctypes.c_void_p]),

@@ -31,6 +31,17 @@ const char *get_error();
         }                                                                               \
     } while (0)
 
+// Returns from the enclosing C-ABI function with GSP_ERR_RCCL on failure (needs <rccl/rccl.h>).
+#define GSP_NCCL(call)                                                                  \
+    do {                                                                                \
+        ncclResult_t gsp_r_ = (call);                                                   \
+        if (gsp_r_ != ncclSuccess) {                                                    \
+            ::gsp::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,         \
+                             ncclGetErrorString(gsp_r_));                               \
+            return GSP_ERR_RCCL;                                                        \
+        }                                                                               \
+    } while (0)
+
 // Device buffer owned by an engine.
 template <typename T>
 struct DevBuf {

@@ -1,8 +1,20 @@
 // gossip_protocol_amd/csrc/pview_engine.cpp -- host side of the PARTIAL-VIEW engine (C ABI).
 //
-// Same tick structure as the full-view engine (scan -> scatter -> tick kernel), with the
-// bounded view table [2][n][V] of 8-byte entries.  Row-sharded multi-GPU operation is
-// provided by row_shard.cpp on top of these pieces.
+// One GPU: per tick, stream-ordered and without host synchronisation,
+//   exclusive_scan(deg) -> off, scatter(out_dst) -> csr, memset(deg), pview_tick_kernel.
+// Row shards (G > 1, BASELINE config 5 on 2/4/8 GPUs): shard g owns the views of nodes
+// [floor(g n / G), floor((g + 1) n / G)).  Before tick t merges, every sender view that a
+// message of tick t - 1 carries to another shard moves there (rowx_kernels.hpp):
+//   pack + gather     pairs (sender, destination shard) and message records, per shard h
+//   counts            all-gather of the 2G pair / record counts of every shard, read by the
+//                     host (the one synchronisation per tick: RCCL needs element counts)
+//   rows + records    RCCL send/recv between every pair of shards inside one group call
+//                     (one process per GPU), or device copies for an in-process group
+//   csr               local messages + received records -> receiver CSR of the local rows
+// then the same tick kernel runs on the local rows, reading remote sender views from the
+// received rows.  Results are identical to the one-GPU engine for every G.
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cstring>
 #include <memory>
@@ -11,22 +23,56 @@
 #include "common.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
+#include "rowx_kernels.hpp"
 #include "scale_kernels.hpp"
 
 namespace gsp {
 std::vector<int32_t> scale_fail_ticks(const gsp_scale_params &p);
 }
 
+namespace {
+
+struct PvShard {
+    int32_t g = 0, row0 = 0, rows = 0;
+    gsp::DevBuf<uint64_t> table[2];
+    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, csr_slot,
+        err, tile_sum;
+    gsp::DevBuf<unsigned long long> dig;
+    // row exchange (G > 1)
+    gsp::DevBuf<int32_t> cnt, cnt_all, recv_msgs, pair_row;
+    gsp::DevBuf<uint64_t> send_rows, recv_rows;
+    gsp::DevBuf<gsp::RowxRec> send_rec, recv_rec;
+
+    void release() {
+        for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
+        for (auto *x : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &csr_slot,
+                        &err, &tile_sum, &cnt, &cnt_all, &recv_msgs, &pair_row})
+            x->release();
+        send_rows.release();
+        recv_rows.release();
+        send_rec.release();
+        recv_rec.release();
+        dig.release();
+    }
+};
+
+}  // namespace
+
 struct gsp_pview {
     gsp_pview_params p{};
     int device = 0;
     hipStream_t st = nullptr;
+    int32_t shards = 1;          // G: row shards of the job
+    int32_t rank = 0;            // first shard held by this engine
+    bool rowmode = false;        // exchange path (G > 1, or any RCCL communicator)
+    ncclComm_t comm = nullptr;
+    int64_t pair_cap = 0, msg_cap = 0;
     int32_t tick = 0;
     bool timing = true;
-    gsp::DevBuf<uint64_t> table[2];
-    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err, tile_sum;
-    gsp::DevBuf<unsigned long long> dig;
+    std::vector<PvShard> local;
     std::vector<int32_t> h_fail;
+    int32_t *h_cnt = nullptr;    // pinned [G][2G]: pair counts then record counts per shard
+    int32_t *h_recv = nullptr;   // pinned [local][G]: records each local shard receives
     struct Timed { hipEvent_t a, b, c; };
     std::vector<Timed> pending;
     std::vector<hipEvent_t> free_events;
@@ -43,11 +89,11 @@ struct gsp_pview {
         return e;
     }
 
-    gsp::PviewTickArgs args(int32_t t) const {
+    gsp::PviewTickArgs args(PvShard &sh, int32_t t) const {
         gsp::PviewTickArgs a{};
-        a.prev = table[(t + 1) & 1].p;
-        a.cur = table[t & 1].p;
-        a.remote = nullptr;
+        a.prev = sh.table[(t + 1) & 1].p;
+        a.cur = sh.table[t & 1].p;
+        a.remote = rowmode ? sh.recv_rows.p : nullptr;
         a.n = p.n;
         a.view = p.view;
         a.inbox = p.inbox;
@@ -56,21 +102,47 @@ struct gsp_pview {
         a.tremove = p.tremove;
         a.drop_pct = p.drop_pct;
         a.h0 = p.h0;
-        a.row0 = 0;
-        a.rows = p.n;
+        a.row0 = sh.row0;
+        a.rows = sh.rows;
         a.seed = p.seed;
-        a.fail_tick = fail_tick.p;
-        a.own_hb = own_hb.p;
-        a.len_prev = len[(t + 1) & 1].p;
-        a.len_cur = len[t & 1].p;
-        a.off = off.p;
-        a.csr_src = csr_src.p;
-        a.csr_slot = nullptr;
-        a.out_dst = out_dst.p;
-        a.deg = deg.p;
-        a.dig = dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
-        a.err = err.p;
+        a.fail_tick = sh.fail_tick.p;
+        a.own_hb = sh.own_hb.p;
+        a.len_cur = sh.len[t & 1].p;
+        a.off = sh.off.p;
+        a.csr_src = sh.csr_src.p;
+        a.csr_slot = rowmode ? sh.csr_slot.p : nullptr;
+        a.out_dst = sh.out_dst.p;
+        a.deg = sh.deg.p;
+        a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
+        a.err = sh.err.p;
         return a;
+    }
+
+    gsp::RowxArgs rowx(PvShard &sh, int32_t t_sent) const {
+        gsp::RowxArgs x{};
+        x.n = p.n;
+        x.shards = shards;
+        x.shard = sh.g;
+        x.fanout = p.fanout;
+        x.row0 = sh.row0;
+        x.rows = sh.rows;
+        x.pair_cap = pair_cap;
+        x.msg_cap = msg_cap;
+        x.row_words = p.view;
+        x.out_dst = sh.out_dst.p;
+        x.table = sh.table[t_sent & 1].p;
+        x.pair_cnt = sh.cnt.p;
+        x.msg_cnt = sh.cnt.p + shards;
+        x.pair_row = sh.pair_row.p;
+        x.send_rows = sh.send_rows.p;
+        x.send_rec = sh.send_rec.p;
+        return x;
+    }
+
+    PvShard *holder(int32_t r) {
+        for (PvShard &sh : local)
+            if (r >= sh.row0 && r < sh.row0 + sh.rows) return &sh;
+        return nullptr;
     }
 };
 
@@ -95,6 +167,130 @@ int pview_validate(const gsp_pview_params *p) {
     return GSP_OK;
 }
 
+int shard_alloc(gsp_pview *s, PvShard &sh) {
+    const int32_t n = s->p.n, F = s->p.fanout, V = s->p.view, G = s->shards;
+    const size_t rows = size_t(sh.rows);
+    hipStream_t st = s->st;
+    for (int b = 0; b < 2; ++b) {
+        GSP_HIP(sh.table[b].alloc(rows * size_t(V)));
+        GSP_HIP(sh.len[b].alloc(rows));
+        GSP_HIP(hipMemsetAsync(sh.len[b].p, 0, rows * 4, st));
+    }
+    GSP_HIP(sh.own_hb.alloc(rows));
+    GSP_HIP(sh.fail_tick.alloc(size_t(n)));
+    GSP_HIP(sh.out_dst.alloc(rows * F));
+    GSP_HIP(sh.deg.alloc(size_t(n)));
+    GSP_HIP(sh.off.alloc(rows + 1));
+    GSP_HIP(sh.fill.alloc(rows));
+    GSP_HIP(sh.csr_src.alloc(size_t(n) * F));      // every message of the job, at most
+    GSP_HIP(sh.err.alloc(1));
+    GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
+    if (s->rowmode) {
+        const size_t G2 = size_t(G);
+        GSP_HIP(sh.csr_slot.alloc(size_t(n) * F));
+        GSP_HIP(sh.cnt.alloc(2 * G2));
+        GSP_HIP(sh.cnt_all.alloc(2 * G2 * G2));
+        GSP_HIP(sh.recv_msgs.alloc(G2));
+        GSP_HIP(sh.pair_row.alloc(G2 * size_t(s->pair_cap)));
+        GSP_HIP(sh.send_rows.alloc(G2 * size_t(s->pair_cap) * size_t(V)));
+        GSP_HIP(sh.recv_rows.alloc(G2 * size_t(s->pair_cap) * size_t(V)));
+        GSP_HIP(sh.send_rec.alloc(G2 * size_t(s->msg_cap)));
+        GSP_HIP(sh.recv_rec.alloc(G2 * size_t(s->msg_cap)));
+        GSP_HIP(hipMemsetAsync(sh.recv_msgs.p, 0, G2 * 4, st));
+    }
+    const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
+    GSP_HIP(sh.dig.alloc(dig));
+    GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * 8, st));
+    GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
+    GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, st));
+    GSP_HIP(hipMemsetAsync(sh.err.p, 0, 4, st));
+    GSP_HIP(hipMemcpyAsync(sh.fail_tick.p, s->h_fail.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
+    return GSP_OK;
+}
+
+// Move the sender views of tick t_sent's cross-shard messages to their destination shards and
+// build every local shard's receiver CSR for tick t_sent + 1.
+int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
+    const int32_t G = s->shards, V = s->p.view, F = s->p.fanout;
+    hipStream_t st = s->st;
+    for (PvShard &sh : s->local) {
+        GSP_HIP(hipMemsetAsync(sh.cnt.p, 0, size_t(2 * G) * 4, st));
+        const gsp::RowxArgs x = s->rowx(sh, t_sent);
+        GSP_HIP(gsp::launch_rowx_pack(x, st));
+        GSP_HIP(gsp::launch_rowx_gather(x, st));
+    }
+    // counts of every shard -> cnt_all[G][2G] (first local shard's copy is read by the host)
+    if (s->comm) {
+        PvShard &sh = s->local[0];
+        GSP_NCCL(ncclAllGather(sh.cnt.p, sh.cnt_all.p, size_t(2 * G), ncclInt32, s->comm, st));
+    } else {
+        for (PvShard &src : s->local)
+            GSP_HIP(hipMemcpyAsync(s->local[0].cnt_all.p + size_t(src.g) * 2 * G, src.cnt.p,
+                                   size_t(2 * G) * 4, hipMemcpyDeviceToDevice, st));
+    }
+    GSP_HIP(hipMemcpyAsync(s->h_cnt, s->local[0].cnt_all.p, size_t(2 * G) * G * 4,
+                           hipMemcpyDeviceToHost, st));
+    GSP_HIP(hipStreamSynchronize(st));
+    auto pairs = [&](int32_t g, int32_t h) { return int64_t(s->h_cnt[size_t(g) * 2 * G + h]); };
+    auto msgs = [&](int32_t g, int32_t h) { return int64_t(s->h_cnt[size_t(g) * 2 * G + G + h]); };
+    const size_t row_bytes = size_t(V) * 8, rec_bytes = sizeof(gsp::RowxRec);
+    double bytes = 0;
+    if (s->comm) {
+        PvShard &sh = s->local[0];
+        const int32_t me = sh.g;
+        GSP_NCCL(ncclGroupStart());
+        for (int32_t h = 0; h < G; ++h) {
+            if (h == me) continue;
+            const size_t so = size_t(h) * size_t(s->pair_cap), mo = size_t(h) * size_t(s->msg_cap);
+            if (pairs(me, h))
+                GSP_NCCL(ncclSend(sh.send_rows.p + so * V, size_t(pairs(me, h)) * V, ncclUint64, h,
+                                  s->comm, st));
+            if (msgs(me, h))
+                GSP_NCCL(ncclSend(sh.send_rec.p + mo, size_t(msgs(me, h)) * 3, ncclInt32, h, s->comm, st));
+            if (pairs(h, me))
+                GSP_NCCL(ncclRecv(sh.recv_rows.p + so * V, size_t(pairs(h, me)) * V, ncclUint64, h,
+                                  s->comm, st));
+            if (msgs(h, me))
+                GSP_NCCL(ncclRecv(sh.recv_rec.p + mo, size_t(msgs(h, me)) * 3, ncclInt32, h, s->comm, st));
+            bytes += double(pairs(me, h)) * row_bytes + double(msgs(me, h)) * rec_bytes;
+        }
+        GSP_NCCL(ncclGroupEnd());
+    } else {
+        for (PvShard &src : s->local)
+            for (PvShard &dst : s->local) {
+                const int32_t g = src.g, h = dst.g;
+                if (g == h) continue;
+                const size_t so = size_t(h) * size_t(s->pair_cap), mo = size_t(h) * size_t(s->msg_cap);
+                const size_t ro = size_t(g) * size_t(s->pair_cap), qo = size_t(g) * size_t(s->msg_cap);
+                if (pairs(g, h))
+                    GSP_HIP(hipMemcpyAsync(dst.recv_rows.p + ro * V, src.send_rows.p + so * V,
+                                           size_t(pairs(g, h)) * row_bytes, hipMemcpyDeviceToDevice, st));
+                if (msgs(g, h))
+                    GSP_HIP(hipMemcpyAsync(dst.recv_rec.p + qo, src.send_rec.p + mo,
+                                           size_t(msgs(g, h)) * rec_bytes, hipMemcpyDeviceToDevice, st));
+                bytes += double(pairs(g, h)) * row_bytes + double(msgs(g, h)) * rec_bytes;
+            }
+    }
+    s->perf.xgmi_bytes += bytes;
+    for (size_t i = 0; i < s->local.size(); ++i) {
+        PvShard &sh = s->local[i];
+        int32_t *hr = s->h_recv + i * size_t(G);
+        for (int32_t h = 0; h < G; ++h) hr[h] = h == sh.g ? 0 : int32_t(msgs(h, sh.g));
+        GSP_HIP(hipMemcpyAsync(sh.recv_msgs.p, hr, size_t(G) * 4, hipMemcpyHostToDevice, st));
+        GSP_HIP(gsp::launch_rowx_recv_deg(sh.recv_rec.p, sh.recv_msgs.p, G, s->msg_cap, sh.row0,
+                                          sh.deg.p, st));
+        GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p + sh.row0, sh.off.p, sh.rows, sh.tile_sum.p, st));
+        GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(sh.rows) * 4, st));
+        GSP_HIP(gsp::launch_rowx_scatter_local(sh.out_dst.p, sh.rows, F, sh.row0, sh.off.p, sh.fill.p,
+                                               sh.csr_src.p, sh.csr_slot.p, st));
+        GSP_HIP(gsp::launch_rowx_scatter_remote(sh.recv_rec.p, sh.recv_msgs.p, G, s->msg_cap,
+                                                s->pair_cap, sh.off.p, sh.fill.p, sh.csr_src.p,
+                                                sh.csr_slot.p, st));
+        GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(s->p.n) * 4, st));
+    }
+    return GSP_OK;
+}
+
 int pview_collect(gsp_pview *s) {
     for (auto &t : s->pending) {
         float a = 0.f, b = 0.f;
@@ -109,9 +305,62 @@ int pview_collect(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     s->pending.clear();
-    int32_t err = 0;
-    GSP_HIP(hipMemcpy(&err, s->err.p, 4, hipMemcpyDeviceToHost));
-    GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY, "a receiver got more than 1024 messages in one tick");
+    for (PvShard &sh : s->local) {
+        int32_t err = 0;
+        GSP_HIP(hipMemcpy(&err, sh.err.p, 4, hipMemcpyDeviceToHost));
+        GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY, "a receiver got more than 1024 messages in one tick");
+    }
+    return GSP_OK;
+}
+
+int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t rank,
+                int32_t local_shards, const void *nccl_id, gsp_pview **out) {
+    GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_pview: out is NULL");
+    *out = nullptr;
+    if (int rc = pview_validate(p)) return rc;
+    GSP_REQUIRE(shards >= 1 && shards <= 64 && shards <= p->n && rank >= 0 &&
+                    rank + local_shards <= shards,
+                GSP_ERR_INVALID, "gsp_pview: shards=%d rank=%d n=%d", shards, rank, p->n);
+    int ndev = 0;
+    GSP_HIP(hipGetDeviceCount(&ndev));
+    GSP_REQUIRE(device >= 0 && device < ndev, GSP_ERR_HIP, "gsp_pview: device %d of %d", device, ndev);
+    GSP_HIP(hipSetDevice(device));
+    std::unique_ptr<gsp_pview> s(new gsp_pview);
+    s->p = *p;
+    s->device = device;
+    s->shards = shards;
+    s->rank = rank;
+    s->rowmode = shards > 1 || nccl_id != nullptr;
+    gsp_scale_params fp{};
+    fp.n = p->n; fp.fail_mode = p->fail_mode; fp.fail_tick = p->fail_tick;
+    fp.fail_ppm = p->fail_ppm; fp.seed = p->seed;
+    s->h_fail = gsp::scale_fail_ticks(fp);
+    int32_t max_rows = 0;
+    for (int32_t g = 0; g < shards; ++g)
+        max_rows = std::max(max_rows, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
+    s->pair_cap = max_rows;                       // a sender row goes to a shard at most once
+    s->msg_cap = int64_t(max_rows) * p->fanout;
+    GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    if (s->rowmode) {
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
+    }
+    if (nccl_id) {
+        ncclUniqueId id;
+        std::memcpy(&id, nccl_id, sizeof id);
+        GSP_NCCL(ncclCommInitRank(&s->comm, shards, id, rank));
+    }
+    s->local.resize(size_t(local_shards));
+    for (int32_t i = 0; i < local_shards; ++i) {
+        PvShard &sh = s->local[size_t(i)];
+        sh.g = rank + i;
+        sh.row0 = gsp::rowx_row0(sh.g, p->n, shards);
+        sh.rows = gsp::rowx_row0(sh.g + 1, p->n, shards) - sh.row0;
+        if (int rc = shard_alloc(s.get(), sh)) return rc;
+    }
+    for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_init(s->args(sh, 0), s->st));
+    GSP_HIP(hipStreamSynchronize(s->st));
+    *out = s.release();
     return GSP_OK;
 }
 
@@ -120,49 +369,29 @@ int pview_collect(gsp_pview *s) {
 extern "C" {
 
 int gsp_pview_create(const gsp_pview_params *p, int device, gsp_pview **out) {
-    GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_pview_create: out is NULL");
-    *out = nullptr;
-    if (int rc = pview_validate(p)) return rc;
-    int ndev = 0;
-    GSP_HIP(hipGetDeviceCount(&ndev));
-    GSP_REQUIRE(device >= 0 && device < ndev, GSP_ERR_HIP, "gsp_pview_create: device %d of %d",
-                device, ndev);
-    GSP_HIP(hipSetDevice(device));
-    std::unique_ptr<gsp_pview> s(new gsp_pview);
-    s->p = *p;
-    s->device = device;
-    gsp_scale_params fp{};
-    fp.n = p->n; fp.fail_mode = p->fail_mode; fp.fail_tick = p->fail_tick;
-    fp.fail_ppm = p->fail_ppm; fp.seed = p->seed;
-    s->h_fail = gsp::scale_fail_ticks(fp);
-    GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
-    const int32_t n = p->n;
-    const size_t tab = size_t(n) * size_t(p->view);
-    for (int b = 0; b < 2; ++b) {
-        GSP_HIP(s->table[b].alloc(tab));
-        GSP_HIP(s->len[b].alloc(size_t(n)));
-        GSP_HIP(hipMemsetAsync(s->len[b].p, 0, size_t(n) * 4, s->st));
+    return pview_build(p, device, 1, 0, 1, nullptr, out);
+}
+
+int gsp_pview_create_group(const gsp_pview_params *p, int device, int32_t shards, gsp_pview **out) {
+    return pview_build(p, device, shards, 0, shards, nullptr, out);
+}
+
+int gsp_pview_create_rank(const gsp_pview_params *p, int device, int32_t rank, int32_t world,
+                          const void *nccl_id, gsp_pview **out) {
+    GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_pview_create_rank: NULL nccl id");
+    return pview_build(p, device, world, rank, 1, nccl_id, out);
+}
+
+int gsp_pview_layout(gsp_pview *s, int32_t *shards, int32_t *rank, int32_t *row0, int32_t *rows) {
+    GSP_REQUIRE(s, GSP_ERR_INVALID, "gsp_pview_layout: NULL");
+    if (shards) *shards = s->shards;
+    if (rank) *rank = s->rank;
+    if (row0) *row0 = s->local[0].row0;
+    if (rows) {
+        int32_t r = 0;
+        for (PvShard &sh : s->local) r += sh.rows;
+        *rows = r;
     }
-    GSP_HIP(s->own_hb.alloc(size_t(n)));
-    GSP_HIP(s->fail_tick.alloc(size_t(n)));
-    GSP_HIP(s->out_dst.alloc(size_t(n) * p->fanout));
-    GSP_HIP(s->deg.alloc(size_t(n)));
-    GSP_HIP(s->off.alloc(size_t(n) + 1));
-    GSP_HIP(s->fill.alloc(size_t(n)));
-    GSP_HIP(s->csr_src.alloc(size_t(n) * p->fanout));
-    GSP_HIP(s->err.alloc(1));
-    GSP_HIP(s->tile_sum.alloc(size_t(n) / 4096 + 1));
-    const size_t dig = size_t(p->max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
-    GSP_HIP(s->dig.alloc(dig));
-    GSP_HIP(hipMemsetAsync(s->dig.p, 0, dig * 8, s->st));
-    GSP_HIP(hipMemsetAsync(s->own_hb.p, 0, size_t(n) * 4, s->st));
-    GSP_HIP(hipMemsetAsync(s->deg.p, 0, size_t(n) * 4, s->st));
-    GSP_HIP(hipMemsetAsync(s->err.p, 0, 4, s->st));
-    GSP_HIP(hipMemcpyAsync(s->fail_tick.p, s->h_fail.data(), size_t(n) * 4, hipMemcpyHostToDevice,
-                           s->st));
-    GSP_HIP(gsp::launch_pview_init(s->args(0), s->st));
-    GSP_HIP(hipStreamSynchronize(s->st));
-    *out = s.release();
     return GSP_OK;
 }
 
@@ -176,11 +405,10 @@ int gsp_pview_destroy(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
-    for (int b = 0; b < 2; ++b) { s->table[b].release(); s->len[b].release(); }
-    for (auto *x : {&s->own_hb, &s->fail_tick, &s->out_dst, &s->deg, &s->off, &s->fill,
-                    &s->csr_src, &s->err, &s->tile_sum})
-        x->release();
-    s->dig.release();
+    for (PvShard &sh : s->local) sh.release();
+    if (s->comm) (void)ncclCommDestroy(s->comm);
+    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->h_recv) (void)hipHostFree(s->h_recv);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -191,7 +419,6 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
     GSP_REQUIRE(s->tick + ticks <= s->p.max_ticks, GSP_ERR_RANGE, "gsp_pview_step: beyond max_ticks");
     GSP_HIP(hipSetDevice(s->device));
     const int32_t n = s->p.n;
-    const int64_t slots = int64_t(n) * s->p.fanout;
     for (int32_t i = 0; i < ticks; ++i) {
         const int32_t t = s->tick + 1;
         gsp_pview::Timed tm{};
@@ -199,13 +426,18 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
             tm = {s->event(), s->event(), s->event()};
             GSP_HIP(hipEventRecord(tm.a, s->st));
         }
-        GSP_HIP(gsp::launch_exclusive_scan(s->deg.p, s->off.p, n, s->tile_sum.p, s->st));
-        GSP_HIP(hipMemsetAsync(s->fill.p, 0, size_t(n) * 4, s->st));
-        GSP_HIP(gsp::launch_scatter(s->out_dst.p, slots, s->p.fanout, 0, s->off.p, s->fill.p,
-                                    s->csr_src.p, s->st));
-        GSP_HIP(hipMemsetAsync(s->deg.p, 0, size_t(n) * 4, s->st));
+        if (s->rowmode) {
+            if (int rc = exchange_and_csr(s, t - 1)) return rc;
+        } else {
+            PvShard &sh = s->local[0];
+            GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
+            GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
+            GSP_HIP(gsp::launch_scatter(sh.out_dst.p, int64_t(n) * s->p.fanout, s->p.fanout, 0,
+                                        sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
+            GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
+        }
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
-        GSP_HIP(gsp::launch_pview_tick(s->args(t), s->st));
+        for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));
         if (s->timing) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);
@@ -227,10 +459,12 @@ int gsp_pview_digest_get(gsp_pview *s, int32_t t, gsp_pview_digest *out) {
     GSP_REQUIRE(s && out && t >= 0 && t <= s->tick, GSP_ERR_INVALID, "gsp_pview_digest_get: tick %d", t);
     if (int rc = gsp_pview_sync(s)) return rc;
     std::vector<unsigned long long> h(size_t(gsp::kPvDigSlots) * gsp::kPvFields);
-    GSP_HIP(hipMemcpy(h.data(), s->dig.p + size_t(t) * h.size(), h.size() * 8, hipMemcpyDeviceToHost));
     unsigned long long f[gsp::kPvFields] = {0};
-    for (int sl = 0; sl < gsp::kPvDigSlots; ++sl)
-        for (int k = 0; k < gsp::kPvFields; ++k) f[k] += h[size_t(sl) * gsp::kPvFields + k];
+    for (PvShard &sh : s->local) {
+        GSP_HIP(hipMemcpy(h.data(), sh.dig.p + size_t(t) * h.size(), h.size() * 8, hipMemcpyDeviceToHost));
+        for (int sl = 0; sl < gsp::kPvDigSlots; ++sl)
+            for (int k = 0; k < gsp::kPvFields; ++k) f[k] += h[size_t(sl) * gsp::kPvFields + k];
+    }
     out->tick = t;
     out->node_rounds = int64_t(f[gsp::kPvRounds]);
     out->merges = int64_t(f[gsp::kPvMerges]);
@@ -248,28 +482,38 @@ int gsp_pview_digest_get(gsp_pview *s, int32_t t, gsp_pview_digest *out) {
 int gsp_pview_row(gsp_pview *s, int32_t r, uint64_t *buf, int32_t cap, int32_t *len) {
     GSP_REQUIRE(s && buf && len && r >= 0 && r < s->p.n && cap >= s->p.view, GSP_ERR_INVALID,
                 "gsp_pview_row: bad argument");
+    PvShard *sh = s->holder(r);
+    GSP_REQUIRE(sh, GSP_ERR_INVALID, "gsp_pview_row: row %d is not held by this rank", r);
     if (int rc = gsp_pview_sync(s)) return rc;
     const int32_t last = std::min(s->tick, s->h_fail[size_t(r)]);
-    GSP_HIP(hipMemcpy(buf, s->table[last & 1].p + size_t(r) * s->p.view, size_t(s->p.view) * 8,
+    const int32_t lr = r - sh->row0;
+    GSP_HIP(hipMemcpy(buf, sh->table[last & 1].p + size_t(lr) * s->p.view, size_t(s->p.view) * 8,
                       hipMemcpyDeviceToHost));
-    GSP_HIP(hipMemcpy(len, s->len[last & 1].p + r, 4, hipMemcpyDeviceToHost));
+    GSP_HIP(hipMemcpy(len, sh->len[last & 1].p + lr, 4, hipMemcpyDeviceToHost));
     return GSP_OK;
 }
 
 int gsp_pview_own_hb(gsp_pview *s, int32_t r, int32_t *hb) {
     GSP_REQUIRE(s && hb && r >= 0 && r < s->p.n, GSP_ERR_INVALID, "gsp_pview_own_hb: bad row");
+    PvShard *sh = s->holder(r);
+    GSP_REQUIRE(sh, GSP_ERR_INVALID, "gsp_pview_own_hb: row %d is not held by this rank", r);
     if (int rc = gsp_pview_sync(s)) return rc;
-    GSP_HIP(hipMemcpy(hb, s->own_hb.p + r, 4, hipMemcpyDeviceToHost));
+    GSP_HIP(hipMemcpy(hb, sh->own_hb.p + (r - sh->row0), 4, hipMemcpyDeviceToHost));
     return GSP_OK;
 }
 
 int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n) {
     GSP_REQUIRE(s && n, GSP_ERR_INVALID, "gsp_pview_messages: NULL");
     if (int rc = gsp_pview_sync(s)) return rc;
-    const int64_t slots = int64_t(s->p.n) * s->p.fanout;
-    *n = slots;
-    if (dst && cap > 0)
-        GSP_HIP(hipMemcpy(dst, s->out_dst.p, size_t(std::min(cap, slots)) * 4, hipMemcpyDeviceToHost));
+    int64_t total = 0;
+    for (PvShard &sh : s->local) {
+        const int64_t slots = int64_t(sh.rows) * s->p.fanout;
+        if (dst && total < cap)
+            GSP_HIP(hipMemcpy(dst + total, sh.out_dst.p, size_t(std::min(cap - total, slots)) * 4,
+                              hipMemcpyDeviceToHost));
+        total += slots;
+    }
+    *n = total;
     return GSP_OK;
 }
 

@@ -123,7 +123,7 @@ struct alignas(16) PvShared {
     uint32_t age_hist[32];
     uint32_t peer_u[16];                 // Philox peer draws of lanes 0..F-1
     int32_t pick[16], chosen[16];
-    int32_t src[kPvMaxInbox], slot[kPvMaxInbox], lenp[kPvMaxInbox], found[kPvMaxInbox];
+    int32_t src[kPvMaxInbox], slot[kPvMaxInbox], found[kPvMaxInbox];
     int32_t misc[8];
     uint32_t wave_scan[4];
     unsigned long long red[4][4];
@@ -171,6 +171,13 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
         sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
         if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
+    }
+    {   // payload entries merged (MP1Node.cpp:245 loop trips): the senders' view sizes
+        uint32_t ne = 0;
+#pragma unroll
+        for (int m = 1; m < kBlocks; ++m) ne += (m <= k && ent[m] != kPvEmpty) ? 1u : 0u;
+        ne = wave_sum32(ne);
+        if (lane == 0 && ne) atomicAdd(reinterpret_cast<uint32_t *>(&sh.misc[5]), ne);
     }
     __syncthreads();
 
@@ -484,15 +491,14 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
     }
     const uint32_t dropped = uint32_t(__popcll(__ballot(drop)));
     if (lane == 0) {
-        a.len_cur[r] = len;
+        a.len_cur[lr] = len;
         if (keff) {
             atomicAdd(&dig[kPvSent], (unsigned long long)keff);
             if (dropped) atomicAdd(&dig[kPvDropped], (unsigned long long)dropped);
         }
         if (!init) {
             a.own_hb[lr] += 1;
-            unsigned long long merges = 0;
-            for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(sh.lenp[j]);
+            const unsigned long long merges = uint64_t(k) + uint64_t(uint32_t(sh.misc[5]));
             atomicAdd(&dig[kPvRounds], 1ull);
             atomicAdd(&dig[kPvMerges], merges);
             atomicAdd(&dig[kPvDelivered], (unsigned long long)k);
@@ -524,6 +530,7 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
         sh.peer_u[tid] = draw_u31(kDomainPeer, a.seed, uint32_t(a.tick), uint32_t(r), uint32_t(tid), 0u);
     if (tid < 32) sh.age_hist[tid] = 0;
     if (tid < kPvMaxInbox) sh.found[tid] = 0;
+    if (tid == 0) sh.misc[5] = 0;
 
     RowOut ro{};
     int32_t k = 0, k_all = 0;
@@ -574,7 +581,6 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
             if (rank < k) {
                 sh.src[rank] = raw[i];
                 sh.slot[rank] = raw_slot[i];
-                sh.lenp[rank] = a.len_prev[raw[i]];            // sender view sizes (merges)
             }
         }
         __syncthreads();

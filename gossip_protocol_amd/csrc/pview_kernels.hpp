@@ -3,7 +3,7 @@
 // HBM layout (BASELINE config 5: n = 1,048,576 nodes, V = 256):
 //   view[2][rows][V]   uint64 entry = id << 32 | hb << 5 | (ts mod 32); ~0 = empty slot.
 //                      Each row is sorted by id with the empty slots last (2 KB at V = 256).
-//   len[2][n]          entries per row (by tick parity)
+//   len[2][rows]       entries per row (by tick parity)
 //   own_hb[rows], fail_tick[n], out_dst[rows * fanout], deg/off/fill/csr_src (receiver CSR)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -28,8 +28,7 @@ struct PviewTickArgs {
     uint64_t seed;
     const int32_t *fail_tick;    // [n]
     int32_t *own_hb;             // [rows]
-    const int32_t *len_prev;     // [n]
-    int32_t *len_cur;            // [n]
+    int32_t *len_cur;            // [rows] view length of this tick
     const int32_t *off;          // [rows + 1]
     const int32_t *csr_src;
     const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)

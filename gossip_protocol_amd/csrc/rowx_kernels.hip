@@ -1,0 +1,149 @@
+// gossip_protocol_amd/csrc/rowx_kernels.hip -- row-sharded gossip exchange kernels (gfx950).
+// See rowx_kernels.hpp for the protocol and the HBM layout.  All of it is integer index
+// work: the only bandwidth that matters is the row gather (2 KB per pair at V = 256), which
+// is a plain coalesced copy.
+#include "rowx_kernels.hpp"
+
+namespace gsp {
+namespace {
+
+constexpr int kMaxFanout = 16;
+
+__global__ void __launch_bounds__(256) rowx_pack_kernel(RowxArgs a) {
+    const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
+    if (lr >= a.rows) return;
+    const int32_t F = a.fanout;
+    int32_t h_of[kMaxFanout], p_of[kMaxFanout];
+#pragma unroll
+    for (int k = 0; k < kMaxFanout; ++k) {
+        h_of[k] = -1;
+        p_of[k] = -1;
+        if (k >= F) continue;
+        const int32_t d = a.out_dst[int64_t(lr) * F + k];
+        if (d < 0) continue;
+        const int32_t h = rowx_owner(d, a.n, a.shards);
+        if (h == a.shard) continue;                   // delivered by the local scatter
+        h_of[k] = h;
+        int32_t p = -1;
+#pragma unroll
+        for (int q = 0; q < kMaxFanout; ++q)          // sender row already bound for h?
+            if (q < k && h_of[q] == h) p = p_of[q];
+        if (p < 0) {
+            p = atomicAdd(&a.pair_cnt[h], 1);
+            a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
+        }
+        p_of[k] = p;
+        const int32_t m = atomicAdd(&a.msg_cnt[h], 1);
+        a.send_rec[int64_t(h) * a.msg_cap + m] =
+            RowxRec{a.row0 + lr, d - rowx_row0(h, a.n, a.shards), p};
+    }
+}
+
+// one wave per pair: copy the sender's row into the destination shard's send region
+__global__ void __launch_bounds__(256) rowx_gather_kernel(RowxArgs a) {
+    const int32_t lane = threadIdx.x & 63;
+    const int64_t w0 = (int64_t(blockIdx.x) * 256 + threadIdx.x) >> 6;
+    const int64_t nw = (int64_t(gridDim.x) * 256) >> 6;
+    const int32_t W = a.row_words;
+    for (int32_t h = 0; h < a.shards; ++h) {
+        const int64_t cnt = a.pair_cnt[h];
+        for (int64_t p = w0; p < cnt; p += nw) {
+            const int32_t lr = a.pair_row[int64_t(h) * a.pair_cap + p];
+            const uint64_t *src = a.table + int64_t(lr) * W;
+            uint64_t *dst = a.send_rows + (int64_t(h) * a.pair_cap + p) * W;
+            for (int32_t i = lane; i < W; i += 64) dst[i] = __builtin_nontemporal_load(src + i);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) rowx_recv_deg_kernel(const RowxRec *rec, const int32_t *cnt,
+                                                            int32_t shards, int64_t msg_cap,
+                                                            int32_t row0, int32_t *deg) {
+    const int64_t i0 = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t step = int64_t(gridDim.x) * 256;
+    for (int32_t h = 0; h < shards; ++h) {
+        const int64_t m = cnt[h];
+        for (int64_t i = i0; i < m; i += step) atomicAdd(&deg[row0 + rec[int64_t(h) * msg_cap + i].dst], 1);
+    }
+}
+
+__global__ void __launch_bounds__(256) rowx_scatter_local_kernel(const int32_t *out_dst, int32_t rows,
+                                                                 int32_t fanout, int32_t row0,
+                                                                 const int32_t *off, int32_t *fill,
+                                                                 int32_t *csr_src, int32_t *csr_slot) {
+    const int64_t slots = int64_t(rows) * fanout;
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < slots;
+         i += int64_t(gridDim.x) * 256) {
+        const int32_t d = out_dst[i] - row0;
+        if (d < 0 || d >= rows) continue;             // none, or another shard's receiver
+        const int32_t pos = off[d] + atomicAdd(&fill[d], 1);
+        const int32_t lr = int32_t(i / fanout);
+        csr_src[pos] = row0 + lr;
+        csr_slot[pos] = lr;
+    }
+}
+
+__global__ void __launch_bounds__(256) rowx_scatter_remote_kernel(const RowxRec *rec, const int32_t *cnt,
+                                                                  int32_t shards, int64_t msg_cap,
+                                                                  int64_t pair_cap, const int32_t *off,
+                                                                  int32_t *fill, int32_t *csr_src,
+                                                                  int32_t *csr_slot) {
+    const int64_t i0 = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    const int64_t step = int64_t(gridDim.x) * 256;
+    for (int32_t h = 0; h < shards; ++h) {
+        const int64_t m = cnt[h];
+        for (int64_t i = i0; i < m; i += step) {
+            const RowxRec r = rec[int64_t(h) * msg_cap + i];
+            const int32_t pos = off[r.dst] + atomicAdd(&fill[r.dst], 1);
+            csr_src[pos] = r.src;
+            csr_slot[pos] = -int32_t(int64_t(h) * pair_cap + r.pair) - 1;
+        }
+    }
+}
+
+unsigned blocks_for(int64_t items, int64_t cap) {
+    int64_t b = (items + 255) / 256;
+    return unsigned(b < 1 ? 1 : (b > cap ? cap : b));
+}
+
+}  // namespace
+
+hipError_t launch_rowx_pack(const RowxArgs &a, hipStream_t st) {
+    if (a.fanout < 1 || a.fanout > kMaxFanout || a.shards < 1 || a.rows < 0) return hipErrorInvalidValue;
+    if (a.rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(rowx_pack_kernel, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowx_gather(const RowxArgs &a, hipStream_t st) {
+    // up to 8 waves per CU-slot worth of pairs; every wave loops over its share
+    const int64_t waves = int64_t(a.rows) * (a.shards - 1);
+    hipLaunchKernelGGL(rowx_gather_kernel, dim3(blocks_for(waves * 64, 8192)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowx_recv_deg(const RowxRec *recv_rec, const int32_t *recv_msgs, int32_t shards,
+                                int64_t msg_cap, int32_t row0, int32_t *deg, hipStream_t st) {
+    hipLaunchKernelGGL(rowx_recv_deg_kernel, dim3(blocks_for(msg_cap, 4096)), dim3(256), 0, st,
+                       recv_rec, recv_msgs, shards, msg_cap, row0, deg);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowx_scatter_local(const int32_t *out_dst, int32_t rows, int32_t fanout,
+                                     int32_t row0, const int32_t *off, int32_t *fill,
+                                     int32_t *csr_src, int32_t *csr_slot, hipStream_t st) {
+    hipLaunchKernelGGL(rowx_scatter_local_kernel, dim3(blocks_for(int64_t(rows) * fanout, 4096)),
+                       dim3(256), 0, st, out_dst, rows, fanout, row0, off, fill, csr_src, csr_slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_rowx_scatter_remote(const RowxRec *recv_rec, const int32_t *recv_msgs,
+                                      int32_t shards, int64_t msg_cap, int64_t pair_cap,
+                                      const int32_t *off, int32_t *fill, int32_t *csr_src,
+                                      int32_t *csr_slot, hipStream_t st) {
+    hipLaunchKernelGGL(rowx_scatter_remote_kernel, dim3(blocks_for(msg_cap, 4096)), dim3(256), 0, st,
+                       recv_rec, recv_msgs, shards, msg_cap, pair_cap, off, fill, csr_src, csr_slot);
+    return hipGetLastError();
+}
+
+}  // namespace gsp

@@ -44,16 +44,6 @@ struct Shard {
     }
 };
 
-#define GSP_NCCL(call)                                                                  \
-    do {                                                                                \
-        ncclResult_t gsp_r_ = (call);                                                   \
-        if (gsp_r_ != ncclSuccess) {                                                    \
-            ::gsp::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #call,         \
-                             ncclGetErrorString(gsp_r_));                               \
-            return GSP_ERR_RCCL;                                                        \
-        }                                                                               \
-    } while (0)
-
 }  // namespace
 
 struct gsp_scale {
@@ -252,6 +242,11 @@ int exchange_picks(gsp_scale *s) {
 
 // message generation for tick t (columns: after the slices are merged)
 int resolve_sends(gsp_scale *s, int32_t t) {
+    // egress per shard of ring collectives: all-gather (G-1)/G of G*n*4 B, all-reduce
+    // 2 (G-1)/G of n*f*4 B
+    const double G = double(s->shards), n = double(s->p.n);
+    s->perf.xgmi_bytes += double(s->local.size()) * (G - 1.0) *
+                          (n * 4.0 + 2.0 * n * s->p.fanout * 4.0 / G);
     if (int rc = exchange_counts(s)) return rc;
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(sh, t), s->st));
     if (int rc = exchange_picks(s)) return rc;

@@ -18,16 +18,38 @@ def unpack_view(entries, length):
 
 
 class PviewEngine:
+    """One partial-view engine.
+
+    group=G (> 1): G row shards inside this process on `device` (exchange by device copies).
+    rank/world/nccl_id: this process holds row shard `rank` of `world` (exchange over RCCL;
+    the id comes from scale.nccl_unique_id() on rank 0).  Default: one GPU, all rows.
+    """
+
     def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
-                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0):
+                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0,
+                 group=1, rank=0, world=1, nccl_id=None):
         self.params = _lib.GspPviewParams(n=n, view=view, fanout=fanout, inbox=inbox,
                                           drop_pct=drop_pct, tremove=tremove, h0=h0,
                                           fail_mode=fail_mode, fail_tick=fail_tick,
                                           fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
         self._h = ctypes.c_void_p()
-        check(lib().gsp_pview_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
-              "gsp_pview_create")
+        P = ctypes.byref
+        if nccl_id is not None:
+            idbuf = ctypes.create_string_buffer(nccl_id, 128)
+            check(lib().gsp_pview_create_rank(P(self.params), device, rank, world, idbuf,
+                                              P(self._h)), "gsp_pview_create_rank")
+        elif group > 1:
+            check(lib().gsp_pview_create_group(P(self.params), device, group, P(self._h)),
+                  "gsp_pview_create_group")
+        else:
+            check(lib().gsp_pview_create(P(self.params), device, P(self._h)), "gsp_pview_create")
         self.n, self.view, self.fanout = n, view, fanout
+
+    def layout(self):
+        """(shards, first shard held, its first row, rows held here)."""
+        v = [ctypes.c_int32() for _ in range(4)]
+        check(lib().gsp_pview_layout(self._h, *[ctypes.byref(x) for x in v]), "gsp_pview_layout")
+        return tuple(x.value for x in v)
 
     def close(self):
         if self._h:

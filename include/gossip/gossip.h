@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 1
+#define GSP_ABI_VERSION 2
 
 typedef enum {
     GSP_OK = 0,
@@ -206,6 +206,8 @@ typedef struct {
     double merge_ms;          /* sum of fused tick-kernel durations (HIP events)      */
     double csr_ms;            /* sum of CSR build kernel durations                    */
     double bytes_per_tick;    /* algorithmic HBM bytes of the fused kernel, last tick  */
+    double xgmi_bytes;        /* bytes this engine's shards sent to other shards, summed
+                                 over ticks (0 on one GPU)                              */
 } gsp_scale_perf;
 
 /* Single-GPU engine on `device` (rows [0, n), full rows, fused tick kernel). */
@@ -277,12 +279,26 @@ typedef struct {
 } gsp_pview_digest;
 
 int gsp_pview_create(const gsp_pview_params *p, int device, gsp_pview **out);
+/* Row-sharded job (DESIGN.md "Partial view, row shards").  Shard g of G owns the views of
+ * nodes [floor(g n / G), floor((g + 1) n / G)); per tick every sender view that a message
+ * carries to another shard moves there once per (sender, shard), with the message records,
+ * by RCCL send/recv (one process per GPU: gsp_pview_create_rank, RCCL id from
+ * gsp_scale_nccl_id) or by device copies (gsp_pview_create_group: every shard inside this
+ * process on one device, for testing the sharded path on one GPU).  Results are identical
+ * to gsp_pview_create for any number of shards. */
+int gsp_pview_create_rank(const gsp_pview_params *p, int device, int32_t rank, int32_t world,
+                          const void *nccl_id, gsp_pview **out);
+int gsp_pview_create_group(const gsp_pview_params *p, int device, int32_t shards, gsp_pview **out);
+/* shards of the job, first shard held here, its first row, rows held by this engine */
+int gsp_pview_layout(gsp_pview *s, int32_t *shards, int32_t *rank, int32_t *row0, int32_t *rows);
 int gsp_pview_destroy(gsp_pview *s);
 int gsp_pview_step(gsp_pview *s, int32_t ticks);
 int gsp_pview_sync(gsp_pview *s);
 int gsp_pview_digest_get(gsp_pview *s, int32_t t, gsp_pview_digest *out);
 /* Row r: `view` packed entries (id << 32 | hb << 5 | ts mod 32, ~0 = empty) and its length. */
 int gsp_pview_row(gsp_pview *s, int32_t r, uint64_t *buf, int32_t cap, int32_t *len);
+/* gsp_pview_row / gsp_pview_own_hb fail with GSP_ERR_INVALID for a row another rank holds;
+ * gsp_pview_messages returns the slots of the rows held here, in row order. */
 int gsp_pview_own_hb(gsp_pview *s, int32_t r, int32_t *hb);
 int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);

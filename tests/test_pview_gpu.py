@@ -69,3 +69,54 @@ def test_pview_matches_oracle(case):
                     sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
                 _cmp_rows(eng, orc, sorted(set(rng.integers(0, n, 40).tolist())))
         _cmp_rows(eng, orc, range(n) if n <= 2000 else range(0, n, 7))
+
+
+SHARD_CASES = [
+    # n, view, fanout, inbox, drop, fail_mode, fail_tick, ppm, seed, ticks, shards
+    (3000, 64, 3, 7, 10, 2, 6, 50000, 5, 20, 2),
+    (2500, 256, 3, 7, 10, 1, 8, 30000, 21, 16, 3),   # uneven shard sizes
+    (1200, 32, 8, 2, 0, 1, 5, 20000, 8, 18, 8),      # 8 shards, inbox overflow
+]
+
+
+@pytest.mark.parametrize("case", SHARD_CASES, ids=lambda c: "n%d_v%d_g%d" % (c[0], c[1], c[-1]))
+def test_pview_row_shards_match_oracle(case):
+    """Row-sharded engine (in-process group: the same pack / gather / CSR kernels as the
+    RCCL path, exchange by device copies) against the oracle: digests every tick, message
+    lists and views periodically, and cross-shard bytes moved."""
+    n, V, f, K, drop, mode, ftick, ppm, seed, ticks, G = case
+    kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+              fail_ppm=ppm, seed=seed)
+    orc = PviewOracle(n, **kw)
+    with PviewEngine(n, max_ticks=ticks, group=G, **kw) as eng:
+        assert eng.layout() == (G, 0, 0, n)
+        eng._tick = 0
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            eng._tick = t
+            assert eng.digest(t) == want, "tick %d" % t
+            if t % 6 == 0:
+                src, dst = orc.messages()
+                m = eng.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+        _cmp_rows(eng, orc, range(n))
+        assert eng.perf()["xgmi_bytes"] > 0
+
+
+def test_pview_rccl_one_rank():
+    """The RCCL code path of the row-sharded engine with a world of one (all-gather of the
+    counts, the send/recv group with no peers) matches the one-GPU engine."""
+    from gossip_protocol_amd.scale import nccl_unique_id
+    n, ticks = 2000, 12
+    kw = dict(view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=1, fail_tick=5,
+              fail_ppm=30000, seed=17, max_ticks=ticks)
+    with PviewEngine(n, **kw) as a, PviewEngine(n, rank=0, world=1, nccl_id=nccl_unique_id(),
+                                                **kw) as b:
+        a.step(ticks)
+        b.step(ticks)
+        for t in range(1, ticks + 1):
+            assert a.digest(t) == b.digest(t)
+        for r in range(0, n, 37):
+            assert a.row(r)[1] == b.row(r)[1] and np.array_equal(a.row(r)[0], b.row(r)[0])
