@@ -7,7 +7,6 @@ sharded engine runs inside libgossip_amd.so on its own RCCL communicator.
 import torch
 import torch.distributed as dist
 
-DIGEST_SUM_FIELDS = ("node_rounds", "merges", "sent", "dropped", "delivered", "joins", "removes")
 
 
 def broadcast_bytes(payload, src=0):
@@ -18,19 +17,21 @@ def broadcast_bytes(payload, src=0):
 
 
 def sum_digests(d):
-    """Job digest from this rank's digest: per-column fields and the event hash are summed
-    over ranks (each rank holds a column slice); per-row fields are counted by rank 0 only,
-    so summing keeps them exact."""
-    vals = [int(d[k]) for k in DIGEST_SUM_FIELDS]
+    """Job digest from this rank's digest: every count is summed over ranks and the event
+    hash is summed modulo 2^64.  Column shards (full view) count per-row quantities on rank
+    0 only and per-column ones on every rank; row shards (partial view) count everything on
+    the rank that owns the row -- either way the sum is the job's digest."""
+    keys = [k for k in d if k not in ("tick", "event_hash")]
+    vals = [int(d[k]) for k in keys]
     t = torch.tensor(vals + [int(d["event_hash"]) & 0xFFFFFFFF, int(d["event_hash"]) >> 32],
                      dtype=torch.int64)
     parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t)
     out = {"tick": d["tick"]}
-    for i, k in enumerate(DIGEST_SUM_FIELDS):
+    for i, k in enumerate(keys):
         out[k] = int(sum(int(p[i]) for p in parts))
-    lo = sum(int(p[len(DIGEST_SUM_FIELDS)]) for p in parts)
-    hi = sum(int(p[len(DIGEST_SUM_FIELDS) + 1]) for p in parts)
+    lo = sum(int(p[len(keys)]) for p in parts)
+    hi = sum(int(p[len(keys) + 1]) for p in parts)
     out["event_hash"] = ((hi << 32) + lo) & 0xFFFFFFFFFFFFFFFF
     return out
 
@@ -41,3 +42,12 @@ def make_rank_engine(n, local_device, **kw):
     rank, world = dist.get_rank(), dist.get_world_size()
     uid = broadcast_bytes(nccl_unique_id() if rank == 0 else None)
     return ScaleEngine(n, device=local_device, rank=rank, world=world, nccl_id=uid, **kw)
+
+
+def make_pview_rank_engine(n, local_device, **kw):
+    """Row shard `rank` of `world` of the partial-view engine, exchange over RCCL."""
+    from .pview import PviewEngine
+    from .scale import nccl_unique_id
+    rank, world = dist.get_rank(), dist.get_world_size()
+    uid = broadcast_bytes(nccl_unique_id() if rank == 0 else None)
+    return PviewEngine(n, device=local_device, rank=rank, world=world, nccl_id=uid, **kw)
