@@ -16,6 +16,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -36,8 +38,8 @@ struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, csr_slot,
-        err, tile_sum;
-    gsp::DevBuf<unsigned long long> dig;
+        err, tile_sum, rc_info, rc_src, rc_slot;
+    gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     // row exchange (G > 1)
     gsp::DevBuf<int32_t> cnt, cnt_all, recv_msgs, pair_row;
     gsp::DevBuf<uint64_t> send_rows, recv_rows;
@@ -46,13 +48,16 @@ struct PvShard {
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
         for (auto *x : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &csr_slot,
-                        &err, &tile_sum, &cnt, &cnt_all, &recv_msgs, &pair_row})
+                        &err, &tile_sum, &cnt, &cnt_all, &recv_msgs, &pair_row, &rc_info, &rc_src,
+                        &rc_slot})
             x->release();
         send_rows.release();
         recv_rows.release();
         send_rec.release();
         recv_rec.release();
         dig.release();
+        prof.release();
+        rowdig.release();
     }
 };
 
@@ -69,6 +74,7 @@ struct gsp_pview {
     int64_t pair_cap = 0, msg_cap = 0;
     int32_t tick = 0;
     bool timing = true;
+    int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail;
     int32_t *h_cnt = nullptr;    // pinned [G][2G]: pair counts then record counts per shard
@@ -108,12 +114,30 @@ struct gsp_pview {
         a.fail_tick = sh.fail_tick.p;
         a.own_hb = sh.own_hb.p;
         a.len_cur = sh.len[t & 1].p;
+        a.rc_info = sh.rc_info.p;
+        a.rc_src = sh.rc_src.p;
+        a.rc_slot = sh.rc_slot.p;
+        a.out_dst = sh.out_dst.p;
+        a.rowdig = sh.rowdig.p;
+        a.deg = sh.deg.p;
+        a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
+        a.err = sh.err.p;
+        a.prof = sh.prof.p;
+        a.waves = waves;
+        return a;
+    }
+
+    gsp::PviewReceiptArgs receipt(PvShard &sh) const {
+        gsp::PviewReceiptArgs a{};
         a.off = sh.off.p;
         a.csr_src = sh.csr_src.p;
         a.csr_slot = rowmode ? sh.csr_slot.p : nullptr;
-        a.out_dst = sh.out_dst.p;
-        a.deg = sh.deg.p;
-        a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
+        a.rows = sh.rows;
+        a.row0 = sh.row0;
+        a.inbox = p.inbox;
+        a.rc_info = sh.rc_info.p;
+        a.rc_src = sh.rc_src.p;
+        a.rc_slot = sh.rc_slot.p;
         a.err = sh.err.p;
         return a;
     }
@@ -185,6 +209,11 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     GSP_HIP(sh.csr_src.alloc(size_t(n) * F));      // every message of the job, at most
     GSP_HIP(sh.err.alloc(1));
     GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
+    GSP_HIP(sh.rc_info.alloc(rows));
+    GSP_HIP(sh.rc_src.alloc(rows * 8));
+    GSP_HIP(sh.rc_slot.alloc(rows * 8));
+    GSP_HIP(sh.rowdig.alloc(rows * 16));
+    GSP_HIP(hipMemsetAsync(sh.rowdig.p, 0, rows * 16 * 8, st));
     if (s->rowmode) {
         const size_t G2 = size_t(G);
         GSP_HIP(sh.csr_slot.alloc(size_t(n) * F));
@@ -200,6 +229,10 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
+    if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
+        GSP_HIP(sh.prof.alloc(64 * gsp::kPvProfPhases));
+        GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * gsp::kPvProfPhases * 8, st));
+    }
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * 8, st));
     GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
     GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, st));
@@ -331,6 +364,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->shards = shards;
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
+    if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
     gsp_scale_params fp{};
     fp.n = p->n; fp.fail_mode = p->fail_mode; fp.fail_tick = p->fail_tick;
     fp.fail_ppm = p->fail_ppm; fp.seed = p->seed;
@@ -405,7 +439,21 @@ int gsp_pview_destroy(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
-    for (PvShard &sh : s->local) sh.release();
+    for (PvShard &sh : s->local) {
+        if (sh.prof.p) {   // GSP_PV_PROFILE diagnostics: cycles per phase, sampled rows
+            std::vector<unsigned long long> h(64 * gsp::kPvProfPhases);
+            if (hipMemcpy(h.data(), sh.prof.p, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                unsigned long long ph[gsp::kPvProfPhases] = {0}, tot = 0;
+                for (size_t i = 0; i < h.size(); ++i) ph[i % gsp::kPvProfPhases] += h[i];
+                for (unsigned long long v : ph) tot += v;
+                std::fprintf(stderr, "pview phases (shard %d, %% of sampled cycles):", sh.g);
+                for (int i = 0; i < gsp::kPvProfPhases; ++i)
+                    std::fprintf(stderr, " p%d=%.1f", i, tot ? 100.0 * double(ph[i]) / double(tot) : 0.0);
+                std::fprintf(stderr, " total=%llu\n", tot);
+            }
+        }
+        sh.release();
+    }
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_recv) (void)hipHostFree(s->h_recv);
@@ -436,6 +484,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
                                         sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
             GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
         }
+        for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));
         if (s->timing) {

@@ -1,24 +1,30 @@
-// gossip_protocol_amd/csrc/pview_kernels.hip -- PARTIAL-VIEW tick kernel for gfx950.
+// gossip_protocol_amd/csrc/pview_kernels.hip -- PARTIAL-VIEW tick kernels for gfx950.
 //
-// One 256-lane workgroup per receiver row; the row's work lives in ~25 KB of LDS (6 rows per
-// CU in flight):
-//   1. receipt order: its <= K smallest senders (canonical order; the rest = inbox overflow);
-//   2. keys: its own view and the k sender views, each a sorted block of 256 slots, as 32-bit
-//      keys id << 11 | source << 8 | slot (source 0 = own view, j = the payload of message j;
-//      the 16-bit value hb << 5 | ts5 stays behind in vals[source][slot]), so equal ids sort
-//      in message order;
+// pview_receipt_kernel (one lane per receiver row): reads the row's CSR segment and keeps its
+//   K smallest senders in ascending order (the canonical receipt order; the rest is inbox
+//   overflow) as a fixed 8-slot record, so the tick kernel reaches the sender views after a
+//   single dependent load instead of three (offsets -> CSR -> rows).
+// pview_tick_kernel (one 256-lane workgroup per receiver row, ~21 KB of LDS):
+//   1. loads: the own view is requested first; the receipt record is read by every wave
+//      (no barrier) and the k sender views follow, one coalesced 2 KB row each;
+//   2. keys: each view is a sorted block of 256 slots of 32-bit keys id << 11 | source << 8
+//      | slot (source 0 = own view, j = the payload of message j; the 16-bit value
+//      hb << 5 | ts5 stays behind in vals[source][slot]), so equal ids sort in message order;
 //   3. union: a tree of merge-path merges (one co-rank binary search per lane per level, then
-//      a register merge of the lane's kBlocks outputs): 256 -> 512 -> 1024 -> 2048 keys, with
-//      the lanes past the (k + 1) * 256 real keys idle;
-//   4. fold: the lane holding the first key of an id folds MP1Node::recvCallBack's rules over
-//      that id's run (own entry, sender event j, payload entry j, ...; MP1Node.cpp:234-301)
-//      and runs the TREMOVE test (MP1Node.cpp:339-348).  A sender found in no list becomes a
-//      new (1, t) entry ("orphan"), adopted by the lane whose key range brackets its id;
+//      a register merge of the lane's kBlocks outputs): 256 -> 512 -> 1024 -> 2048 keys;
+//   4. fold, in registers: each lane walks its kBlocks keys once, folding MP1Node::
+//      recvCallBack's rules over every id run whose first key it holds (own entry, then for
+//      j = 1..k the sender event of message j and payload entry j; MP1Node.cpp:234-301) and
+//      the TREMOVE test (MP1Node.cpp:339-348); a run that continues into the next lane's
+//      keys is finished from LDS.  A sender found in no list becomes a new (1, t) entry
+//      ("orphan"); the lane whose id bracket holds it is the one that would hold its key,
+//      so found / not found is decided locally;
 //   5. survivors compacted in id order (one block scan); eviction to V by (age, -hb, id) with
 //      an age histogram, an hb histogram of the boundary age and an id-order tie prefix, all
-//      resolved by a single packed block scan;
+//      resolved by a single packed block scan over the lanes' survivors (kept in registers);
 //   6. the new sorted view is written back (2 KB, coalesced); Philox rank-select picks the
-//      peers (draws precomputed by lanes 0..F-1, drop draws in parallel).
+//      peers; the row's digest counts go to a per-row record (no global atomics), summed by
+//      pview_digest_kernel.
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include "philox.hpp"
 #include "pview_kernels.hpp"
@@ -29,8 +35,8 @@ namespace {
 constexpr int kSlots = kPvMaxView;                    // slots per source block
 constexpr int kMaxBlocks = kPvMaxInbox + 1;           // own view + K sender views
 constexpr int kMaxKeys = kSlots * kMaxBlocks;         // 2048
-constexpr int kUCap = kMaxKeys + 8;                   // survivors + orphans
 constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: above every node id
+constexpr uint32_t kNoId = 0xFFFFFFFFu;
 static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
 
 __device__ inline uint64_t pv_event_mix(uint32_t kind, uint32_t t, uint32_t r, uint32_t x) {
@@ -48,6 +54,8 @@ __device__ inline uint32_t pv_merge(uint32_t e, uint32_t v, uint32_t t5, uint32_
     const uint32_t add = (v != 0u && ((t5 - v) & 31u) < tr) ? v : 0u;
     return e ? upd : add;
 }
+// the sender entry of a GOSSIP: hb + 1 and ts = t, or (1, t) when absent (MP1Node.cpp:237-243)
+__device__ inline uint32_t pv_event(uint32_t v, uint32_t t5) { return (((v >> 5) + 1u) << 5) | t5; }
 
 __device__ inline uint32_t key_id(uint32_t k) { return k >> 11; }
 __device__ inline uint32_t key_src(uint32_t k) { return (k >> 8) & 7u; }
@@ -64,7 +72,9 @@ __device__ inline uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// exclusive block scan over the 256 lanes (fenced by barriers); *total = sum of all lanes
+// exclusive block scan over the 256 lanes; *total = sum of all lanes.  One barrier: the
+// caller alternates between two s_wave buffers, so a buffer is rewritten only after a later
+// scan's barrier has retired every read of it.
 __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_wave) {
     const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t incl = v;
@@ -73,7 +83,6 @@ __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_w
         const uint32_t u = __shfl_up(incl, d, 64);
         if (lane >= d) incl += u;
     }
-    __syncthreads();
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
     uint32_t before = 0, all = 0;
@@ -116,70 +125,93 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
     }
 }
 
+// LDS of one row (20 KB: 8 rows per CU).  keys[cur] (the sorted union C) is dead once the
+// fold is done and then holds: the kept ids W [0, 256), the kept values (u16) at word 512,
+// the boundary-age hb histogram (2048 u16 bins) at words [1024, 2048).  keys[cur ^ 1] (the
+// last merge level's source) is dead after the tree and holds the age histogram (words
+// [0, 32)), the block-scan buffers (words [2040, 2048)) and, when no eviction is needed,
+// the survivor ids U (words [0, 256)).
 struct alignas(16) PvShared {
-    uint32_t keys[2][kUCap];             // merge ping-pong; then survivor ids (U), kept ids (W)
-    uint16_t vals[kMaxKeys];             // values by (source, slot); then hb histogram; then W vals
-    uint16_t uval[kUCap];                // survivor values
-    uint32_t age_hist[32];
-    uint32_t peer_u[16];                 // Philox peer draws of lanes 0..F-1
-    int32_t pick[16], chosen[16];
-    int32_t src[kPvMaxInbox], slot[kPvMaxInbox], found[kPvMaxInbox];
-    int32_t misc[8];
-    uint32_t wave_scan[4];
-    unsigned long long red[4][4];
+    uint32_t keys[2][kMaxKeys];          // merge ping-pong; then the regions above
+    uint16_t vals[kMaxKeys];             // values by (source, slot); then survivor values
+};
+constexpr int kWValWord = 512, kHistWord = 1024;
+
+__device__ inline int32_t lds_word(const PvShared &sh, const uint32_t *p) {
+    return int32_t(p - &sh.keys[0][0]);
+}
+__device__ inline int32_t lds_half(const PvShared &sh, const void *p) {
+    return int32_t(reinterpret_cast<const uint16_t *>(p) - reinterpret_cast<const uint16_t *>(&sh));
+}
+
+// Diagnostics (GSP_PV_PROFILE=1): thread 0 of every 16th row adds the cycles since the last
+// mark to prof[slot][phase]; a scalar branch on a kernel argument when off.
+struct PvMark {
+    unsigned long long *out = nullptr;
+    uint64_t last = 0;
+    __device__ __forceinline__ void init(unsigned long long *prof) {
+        if (prof && threadIdx.x == 0 && (blockIdx.x & 15u) == 0) {
+            out = prof + (blockIdx.x >> 4 & 63u) * kPvProfPhases;
+            last = clock64();
+        }
+    }
+    __device__ __forceinline__ void mark(int phase) {
+        if (out) {
+            const uint64_t now = clock64();
+            atomicAdd(out + phase, (unsigned long long)(now - last));
+            last = now;
+        }
+    }
 };
 
+// The final view: ids and values as LDS offsets (words of keys[][], u16 units of the whole
+// PvShared) -- plain integers, so the row's state never leaves registers.
 struct RowOut {
-    const uint32_t *ids;
-    const uint16_t *vals;
+    int32_t ids_off, vals_off;
     int32_t len;
-    uint32_t joins, removes, evicts;
+    uint32_t joins, removes, evicts, merged;
     uint64_t hsum;
 };
 
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 4 or 8).
+// ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
 template <int kBlocks>
-__device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t lr,
-                                             int32_t r, int32_t k, RowOut &ro) {
+__device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
+                                             int32_t k, uint64_t ent0,
+                                             const uint32_t (&ssrc)[kPvMaxInbox],
+                                             const int32_t (&sslot)[kPvMaxInbox], RowOut &ro,
+                                             PvMark &pm) {
     constexpr int Q = kBlocks;                           // keys per lane
     constexpr int P = kBlocks * kSlots;
-    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t tid = threadIdx.x;
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
     const int32_t Pe = (k + 1) * kSlots;                // keys that can be real
 
     // ---- 2. keys: one sorted block of 256 slots per source -----------------------------------
-    // every row load is issued before any is consumed (one HBM round trip, not k + 1)
     uint64_t ent[kBlocks];
+    ent[0] = ent0;
 #pragma unroll
-    for (int m = 0; m < kBlocks; ++m) {
+    for (int m = 1; m < kBlocks; ++m) {
         ent[m] = kPvEmpty;
         if (m <= k && tid < V) {
-            const uint64_t *row;
-            if (m == 0) row = a.prev + int64_t(lr) * V;
-            else {
-                const int32_t sl = sh.slot[m - 1];
-                row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
-            }
+            const int32_t sl = sslot[m - 1];
+            const uint64_t *row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
             ent[m] = __builtin_nontemporal_load(row + tid);
         }
     }
+    uint32_t merged = 0;                                 // payload entries (MP1Node.cpp:245 trips)
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
         const bool ok = ent[m] != kPvEmpty;
+        merged += (m >= 1 && ok) ? 1u : 0u;
         sh.keys[0][m * kSlots + tid] =
             ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
         sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
         if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
     }
-    {   // payload entries merged (MP1Node.cpp:245 loop trips): the senders' view sizes
-        uint32_t ne = 0;
-#pragma unroll
-        for (int m = 1; m < kBlocks; ++m) ne += (m <= k && ent[m] != kPvEmpty) ? 1u : 0u;
-        ne = wave_sum32(ne);
-        if (lane == 0 && ne) atomicAdd(reinterpret_cast<uint32_t *>(&sh.misc[5]), ne);
-    }
     __syncthreads();
+    pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
     const int32_t beg = tid * Q;
@@ -216,139 +248,147 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         cur ^= 1;
     }
     const uint32_t *C = sh.keys[cur];
+    uint32_t *const age_hist = sh.keys[cur ^ 1];              // dead after the tree
+    uint32_t *const scan_buf = sh.keys[cur ^ 1] + 2040;
+    if (tid < 32) age_hist[tid] = 0;
 
-    // ---- 4. fold each id's run ------------------------------------------------------------
-    uint32_t ck[Q];
+    pm.mark(2);
+    // ---- 4. fold every id run that starts in this lane, in registers ------------------------
+    uint32_t ck[Q], vv[Q];
     lds_load<Q>(C + beg, ck);
-    const uint32_t lo_id = tid > 0 ? key_id(C[beg - 1]) + 1u : 0u;  // this lane brackets ids
-    const uint32_t hi_id = tid < kPvBlock - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
-    uint32_t ssrc[kPvMaxInbox];
+    const uint32_t prev_key = tid > 0 ? C[beg - 1] : 0u;
+    const uint32_t next_key = beg + Q < P ? C[beg + Q] : kKeyMax;
 #pragma unroll
-    for (int jj = 0; jj < kPvMaxInbox; ++jj) ssrc[jj] = jj < k ? uint32_t(sh.src[jj]) : kKeyMax;
+    for (int e = 0; e < Q; ++e)                                // value gathers, all in flight
+        vv[e] = ck[e] != kKeyMax ? uint32_t(sh.vals[key_src(ck[e]) * kSlots + key_slot(ck[e])]) : 0u;
+    const uint32_t lo_id = tid > 0 ? key_id(prev_key) + 1u : 0u;   // this lane brackets ids
+    const uint32_t hi_id = tid < kPvBlock - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
 
     uint32_t res[Q], rid[Q];
     uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
     uint64_t hsum = 0;
+    // the run being folded: id, value, own-view value, sender event (message index, applied)
+    uint32_t ax = kNoId, av = 0, ae0 = 0, ajs = 0;
+    bool aown = false, adone = false;
 #pragma unroll
     for (int e = 0; e < Q; ++e) {
         res[e] = 0;
         rid[e] = 0;
-        const uint32_t kk0 = ck[e];
-        const uint32_t x = key_id(kk0);
-        const bool first = e == 0 ? x >= lo_id : x != key_id(ck[e - 1]);
-        if (kk0 == kKeyMax || !first) continue;
-        int32_t jsend = 0;
+        const uint32_t key = ck[e];
+        if (key == kKeyMax) continue;
+        const uint32_t x = key_id(key), src = key_src(key);
+        if (x != ax) {                                         // a run starts at key e
+            ax = x;
+            aown = e > 0 || x >= lo_id;                        // else the previous lane's run
+            av = ae0 = 0;
+            ajs = 0;
 #pragma unroll
-        for (int jj = 0; jj < kPvMaxInbox; ++jj) jsend = ssrc[jj] == x ? jj + 1 : jsend;
-        if (jsend) found_mask |= 1u << (jsend - 1);
-        if (x == uint32_t(r)) continue;                       // never list yourself
-        int32_t pos = beg + e;
-        uint32_t nk = kk0, v = 0, e0 = 0;
-        if (key_src(nk) == 0) {
-            e0 = v = sh.vals[key_slot(nk)];
-            ++pos;
-            nk = pos < Pe ? C[pos] : kKeyMax;
+            for (int jj = 0; jj < kPvMaxInbox; ++jj) ajs = ssrc[jj] == x ? uint32_t(jj + 1) : ajs;
+            adone = false;
+            if (aown && ajs) found_mask |= 1u << (ajs - 1);
         }
-        for (int32_t jj = 1; jj <= k; ++jj) {
-            if (jj == jsend) v = (((v >> 5) + 1u) << 5) | t5;              // MP1Node.cpp:237-243
-            if (key_id(nk) == x && key_src(nk) == uint32_t(jj)) {
-                v = pv_merge(v, sh.vals[jj * kSlots + key_slot(nk)], t5, tr);  // MP1Node.cpp:247-301
+        if (src == 0) {
+            av = ae0 = vv[e];
+        } else {
+            if (ajs && !adone && ajs < src) { av = pv_event(av, t5); adone = true; }
+            av = pv_merge(av, vv[e], t5, tr);
+        }
+        // does the run end here?
+        uint32_t nxt = e + 1 < Q ? ck[e + 1 < Q ? e + 1 : e] : next_key;
+        if (e + 1 == Q && nxt != kKeyMax && key_id(nxt) == x) {   // continues into the next lane
+            int32_t pos = beg + Q;
+            while (pos < P) {
+                const uint32_t kk = C[pos];
+                if (kk == kKeyMax || key_id(kk) != x) break;
+                const uint32_t s2 = key_src(kk);
+                if (ajs && !adone && ajs < s2) { av = pv_event(av, t5); adone = true; }
+                av = pv_merge(av, sh.vals[s2 * kSlots + key_slot(kk)], t5, tr);
                 ++pos;
-                nk = pos < Pe ? C[pos] : kKeyMax;
             }
+            nxt = kKeyMax;
         }
-        if (!v) continue;
-        if (!e0) { joins++; hsum += pv_event_mix(1, t, uint32_t(r), x); }
-        if (((t5 - v) & 31u) >= tr) {                          // TREMOVE scan
+        if (nxt != kKeyMax && key_id(nxt) == x) continue;
+        if (!aown) continue;
+        if (ajs && !adone) av = pv_event(av, t5);
+        if (x == uint32_t(r) || !av) continue;                  // never list yourself
+        if (!ae0) { joins++; hsum += pv_event_mix(1, t, uint32_t(r), x); }
+        if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
             hsum += pv_event_mix(2, t, uint32_t(r), x);
             continue;
         }
-        res[e] = v;
+        res[e] = av;
         rid[e] = x;
         nloc++;
     }
-    // candidate orphans: senders whose id falls in this lane's bracket
+    // orphans: senders in this lane's bracket that no list holds (their key would be here)
     uint32_t adopt = 0;
     int32_t ains[kPvMaxInbox];
 #pragma unroll
     for (int jj = 0; jj < kPvMaxInbox; ++jj) {
         ains[jj] = 0;
         const uint32_t x = ssrc[jj];
-        if (jj < k && x >= lo_id && x <= hi_id && beg <= Pe) {
+        if (jj < k && x >= lo_id && x <= hi_id && beg <= Pe && !((found_mask >> jj) & 1u)) {
             int32_t c = 0;
 #pragma unroll
             for (int e = 0; e < Q; ++e) c += key_id(ck[e]) < x ? 1 : 0;
             ains[jj] = c;
             adopt |= 1u << jj;
-        }
-    }
-    if (found_mask) {
-#pragma unroll
-        for (int jj = 0; jj < kPvMaxInbox; ++jj)
-            if ((found_mask >> jj) & 1u) sh.found[jj] = 1;
-    }
-    __syncthreads();
-    if (adopt) {
-#pragma unroll
-        for (int jj = 0; jj < kPvMaxInbox; ++jj) {
-            if (!((adopt >> jj) & 1u)) continue;
-            if (sh.found[jj]) { adopt &= ~(1u << jj); continue; }
             nloc++;
             joins++;
-            hsum += pv_event_mix(1, t, uint32_t(r), ssrc[jj]);
+            hsum += pv_event_mix(1, t, uint32_t(r), x);
         }
     }
 
+    pm.mark(3);
     // ---- 5a. survivors (and adopted orphans), compacted in id order -------------------------
-    uint32_t total = 0;
-    const uint32_t base = block_scan(nloc, &total, sh.wave_scan);
-    uint32_t *Uid = sh.keys[cur ^ 1];
-    uint16_t *Uval = sh.uval;
-    const bool evict = int32_t(total) > V;
-    {
-        uint32_t w = base;
+    // for_each visits this lane's survivors in id order as (value, id)
+    const uint32_t fresh = (1u << 5) | t5;                     // an orphan: (hb 1, ts t)
+    auto for_each = [&](auto &&f) {
         if (!adopt) {
 #pragma unroll
             for (int e = 0; e < Q; ++e)
-                if (res[e]) {
-                    Uid[w] = rid[e];
-                    Uval[w] = uint16_t(res[e]);
-                    if (evict) atomicAdd(&sh.age_hist[(t5 - res[e]) & 31u], 1u);
-                    w++;
-                }
+                if (res[e]) f(res[e], rid[e]);
         } else {
-            const uint32_t fresh = (1u << 5) | t5;             // an orphan: (hb 1, ts t)
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
 #pragma unroll
                 for (int jj = 0; jj < kPvMaxInbox; ++jj)
-                    if (((adopt >> jj) & 1u) && ains[jj] == e) {
-                        Uid[w] = ssrc[jj];
-                        Uval[w] = uint16_t(fresh);
-                        if (evict) atomicAdd(&sh.age_hist[0], 1u);
-                        w++;
-                    }
-                if (e < Q && res[e]) {
-                    Uid[w] = rid[e];
-                    Uval[w] = uint16_t(res[e]);
-                    if (evict) atomicAdd(&sh.age_hist[(t5 - res[e]) & 31u], 1u);
-                    w++;
-                }
+                    if (((adopt >> jj) & 1u) && ains[jj] == e) f(fresh, ssrc[jj]);
+                if (e < Q && res[e]) f(res[e], rid[e]);
             }
         }
+    };
+    uint32_t total = 0;
+    const uint32_t base = block_scan(nloc, &total, scan_buf);
+    const bool evict = int32_t(total) > V;
+    uint32_t *hist = sh.keys[cur] + kHistWord;                // 2048 hb bins, u16 pairs; C is dead
+    if (!evict) {                                              // the survivors are the view
+        uint32_t *Uid = sh.keys[cur ^ 1];
+        uint16_t *Uval = sh.vals;                              // the gathered values are dead
+        uint32_t w = base;
+        for_each([&](uint32_t v, uint32_t x) {
+            Uid[w] = x;
+            Uval[w] = uint16_t(v);
+            w++;
+        });
+        ro.ids_off = lds_word(sh, Uid);
+        ro.vals_off = lds_half(sh, Uval);
+        ro.len = int32_t(total);
+    } else {
+        for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
+        for_each([&](uint32_t v, uint32_t) { atomicAdd(&age_hist[(t5 - v) & 31u], 1u); });
     }
-    ro.ids = Uid;
-    ro.vals = Uval;
-    ro.len = int32_t(total);
 
+    pm.mark(4);
     // ---- 5b. eviction to V by (age, -hb, id) ------------------------------------------------
     if (evict) {
-        uint32_t *hist = reinterpret_cast<uint32_t *>(sh.vals);   // 2048 hb bins, u16 pairs
-        for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
-        __syncthreads();
-        if (wave == 0) {                                   // boundary age: first cum >= V
-            const uint32_t hv = lane < 32 ? sh.age_hist[lane] : 0u;
+        __syncthreads();                                   // age histogram complete, hist zeroed
+        // boundary age astar: first cumulative count >= V (every wave computes it)
+        const int32_t lane = tid & 63;
+        uint32_t astar, need, at;
+        {
+            const uint32_t hv = lane < 32 ? age_hist[lane] : 0u;
             uint32_t incl = hv;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
@@ -357,181 +397,150 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             }
             const unsigned long long hit = __ballot(lane < 32 && incl >= uint32_t(V));
             const int32_t ab = __builtin_ffsll(hit) - 1;
-            const uint32_t before = __shfl(incl - hv, ab, 64);
-            const uint32_t at = __shfl(hv, ab, 64);
-            if (lane == 0) {
-                sh.misc[0] = ab;
-                sh.misc[1] = V - int32_t(before);          // kept at the boundary age
-                sh.misc[2] = int32_t(at);
-            }
+            astar = uint32_t(ab);
+            need = uint32_t(V) - __shfl(incl - hv, ab, 64);    // kept at the boundary age
+            at = __shfl(hv, ab, 64);
         }
-        __syncthreads();
-        const uint32_t astar = uint32_t(sh.misc[0]);
-        const int32_t need = sh.misc[1];
-        const bool tie = sh.misc[2] > need;
-        uint32_t hstar = 0;
-        int32_t need2 = 0;
+        pm.mark(7);
+        const bool tie = at > need;
+        uint32_t hstar = 0, need2 = 0;
         if (tie) {                                         // boundary hb among age == astar
-            for (uint32_t i = base; i < base + nloc; ++i) {
-                const uint32_t v = Uval[i];
+            for_each([&](uint32_t v, uint32_t) {
                 if (((t5 - v) & 31u) == astar)
                     atomicAdd(&hist[(v >> 5) >> 1], 1u << (((v >> 5) & 1u) * 16u));
-            }
+            });
             __syncthreads();
-            // lane t owns hb bins 2047 - 8t - 7 .. 2047 - 8t (descending order of lanes)
-            const uint16_t *h16 = sh.vals;
+            // every wave: lane l sums hb bins 2047 - 32l - 31 .. 2047 - 32l (descending lanes),
+            // the lane holding the need-th largest walks its bins
+            const uint16_t *h16 = reinterpret_cast<const uint16_t *>(hist);
+            const uint4 *hw = reinterpret_cast<const uint4 *>(hist + 1024 - 16 * (lane + 1));
             uint32_t loc = 0;
 #pragma unroll
-            for (int b = 0; b < 8; ++b) loc += h16[2047 - 8 * tid - b];
-            uint32_t tot = 0;
-            const uint32_t ex = block_scan(loc, &tot, sh.wave_scan);
-            if (ex < uint32_t(need) && uint32_t(need) <= ex + loc) {
-                uint32_t cum = ex;
-                for (int b = 0; b < 8; ++b) {
-                    const int32_t h = 2047 - 8 * tid - b;
+            for (int q = 0; q < 4; ++q) {
+                const uint4 x = hw[q];
+                loc += (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
+                       (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
+            }
+            uint32_t incl = loc;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t u = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += u;
+            }
+            const unsigned long long hit = __ballot(incl >= need);
+            const int32_t lb = __builtin_ffsll(hit) - 1;
+            uint32_t hs = 0, n2 = 0;
+            if (lane == lb) {
+                uint32_t cum = incl - loc;
+                for (int b = 0; b < 32; ++b) {
+                    const int32_t h = 2047 - 32 * lane - b;
                     const uint32_t c = h16[h];
-                    if (cum + c >= uint32_t(need)) {
-                        sh.misc[3] = h;
-                        sh.misc[4] = need - int32_t(cum);  // kept among (astar, h) ties
-                        break;
-                    }
+                    if (cum + c >= need) { hs = uint32_t(h); n2 = need - cum; break; }
                     cum += c;
                 }
             }
-            __syncthreads();
-            hstar = uint32_t(sh.misc[3]);
-            need2 = sh.misc[4];
+            hstar = __shfl(hs, lb, 64);
+            need2 = __shfl(n2, lb, 64);                        // kept among (astar, hstar) ties
         }
+        pm.mark(8);
         // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
         uint32_t nt = 0, nk = 0;
-        for (uint32_t i = base; i < base + nloc; ++i) {
-            const uint32_t v = Uval[i], age = (t5 - v) & 31u, hb = v >> 5;
+        for_each([&](uint32_t v, uint32_t) {
+            const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
             const bool is_tie = tie && age == astar && hb == hstar;
             nt += is_tie ? 1u : 0u;
             nk += (!is_tie && (age < astar || (age == astar && (!tie || hb > hstar)))) ? 1u : 0u;
-        }
+        });
         uint32_t sums = 0;
-        const uint32_t ex = block_scan(nt | (nk << 16), &sums, sh.wave_scan);
+        const uint32_t ex = block_scan(nt | (nk << 16), &sums, scan_buf + 4);
         uint32_t tie_before = ex & 0xFFFFu;
-        const uint32_t ties_kept_before = tie_before < uint32_t(need2) ? tie_before : uint32_t(need2);
+        const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
-        uint32_t *Wid = sh.keys[cur];                       // C is dead
-        uint16_t *Wval = sh.vals;                           // the histogram is dead
-        for (uint32_t i = base; i < base + nloc; ++i) {
-            const uint32_t v = Uval[i], age = (t5 - v) & 31u, hb = v >> 5;
+        uint32_t *Wid = sh.keys[cur];
+        uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
+        for_each([&](uint32_t v, uint32_t x) {
+            const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
             bool keep = age < astar || (age == astar && (!tie || hb > hstar));
-            if (tie && age == astar && hb == hstar) keep = int32_t(tie_before++) < need2;
+            if (tie && age == astar && hb == hstar) keep = tie_before++ < need2;
             if (keep) {
-                Wid[w] = Uid[i];
+                Wid[w] = x;
                 Wval[w] = uint16_t(v);
                 w++;
             } else {
                 evicts++;
-                hsum += pv_event_mix(3, t, uint32_t(r), Uid[i]);
+                hsum += pv_event_mix(3, t, uint32_t(r), x);
             }
-        }
-        ro.ids = Wid;
-        ro.vals = Wval;
+        });
+        ro.ids_off = lds_word(sh, Wid);
+        ro.vals_off = lds_half(sh, Wval);
         ro.len = V;
     }
     ro.joins = joins;
     ro.removes = removes;
     ro.evicts = evicts;
+    ro.merged = merged;
     ro.hsum = hsum;
     __syncthreads();
 }
 
-// ---- 6. write the view, heartbeat, digest, sends ------------------------------------------
+// ---- 6. write the view and the row's digest record (peers: pview_send_kernel) -------------
+// rowdig[lr][wave][4]: w0 = merges | delivered << 32 | sent << 40 | dropped << 48 | round << 56,
+// w1 = joins | removes << 16 | evicts << 32 | overflow << 48, w2 = event hash, w3 = 0; each
+// wave writes its own partial record (no barrier); sent / dropped come from the send kernel.
 __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, int32_t lr,
-                                          int32_t r, int32_t k, int32_t k_all, bool init,
-                                          const RowOut &ro) {
+                                          int32_t k, int32_t k_all, bool init, const RowOut &ro) {
     const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int32_t V = a.view, F = a.fanout, len = ro.len;
+    const int32_t V = a.view, len = ro.len;
     const uint32_t t = uint32_t(a.tick);
+    const uint32_t *ids = &sh.keys[0][0] + ro.ids_off;
+    const uint16_t *vals = reinterpret_cast<const uint16_t *>(&sh) + ro.vals_off;
     uint64_t *out = a.cur + int64_t(lr) * V;
     for (int32_t i = tid; i < V; i += kPvBlock)
         __builtin_nontemporal_store(
-            i < len ? (uint64_t(ro.ids[i]) << 32) | uint64_t(ro.vals[i]) : kPvEmpty, out + i);
-
-    unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
-    if (!init) {
-        const uint32_t j = wave_sum32(ro.joins), rm = wave_sum32(ro.removes), ev = wave_sum32(ro.evicts);
-        const uint64_t h = wave_sum64(ro.hsum);
-        if (lane == 0) { sh.red[wave][0] = j; sh.red[wave][1] = rm; sh.red[wave][2] = ev; sh.red[wave][3] = h; }
-        __syncthreads();
+            i < len ? (uint64_t(ids[i]) << 32) | uint64_t(vals[i]) : kPvEmpty, out + i);
+    if (init) {
+        if (tid == 0) a.len_cur[lr] = len;
+        return;
     }
-    if (wave != 0) return;
-    // peers: min(F, len) distinct members by Philox rank-select over the id order
-    const int32_t keff = F < len ? F : len;
+    const uint64_t jr = wave_sum32(ro.joins) | (uint64_t(wave_sum32(ro.removes)) << 16);
+    const uint64_t ev = wave_sum32(ro.evicts);
+    uint64_t mg = wave_sum32(ro.merged);
+    const uint64_t h = wave_sum64(ro.hsum);
     if (lane == 0) {
-        int32_t nch = 0;
-        for (int32_t kk = 0; kk < keff; ++kk) {
-            int32_t rk = int32_t(sh.peer_u[kk] % uint32_t(len - kk));
-            int32_t pos = 0;
-            while (pos < nch && rk >= sh.chosen[pos]) { rk++; pos++; }
-            for (int32_t q2 = nch; q2 > pos; --q2) sh.chosen[q2] = sh.chosen[q2 - 1];
-            sh.chosen[pos] = rk;
-            nch++;
-            sh.pick[kk] = int32_t(ro.ids[rk]);
+        uint64_t w0 = mg, w1 = jr | (ev << 32);
+        if (wave == 0) {
+            a.len_cur[lr] = len;
+            a.own_hb[lr] = int32_t(t);               // alive at every tick 1..t (pre-joined)
+            w0 += uint64_t(k) | (uint64_t(k) << 32) | (1ull << 56);
+            w1 |= uint64_t(k_all - k) << 48;
         }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    bool drop = false;
-    if (lane < F) {
-        int32_t dst = -1;
-        if (lane < keff) {
-            dst = sh.pick[lane];
-            const uint32_t dr = draw_u31(kDomainSend, a.seed, t, uint32_t(r), uint32_t(dst), 3u);
-            if (int32_t(dr % 100u) < a.drop_pct) { drop = true; dst = -1; }
-        }
-        a.out_dst[int64_t(lr) * F + lane] = dst;
-        if (dst >= 0) atomicAdd(&a.deg[dst], 1);
-    }
-    const uint32_t dropped = uint32_t(__popcll(__ballot(drop)));
-    if (lane == 0) {
-        a.len_cur[lr] = len;
-        if (keff) {
-            atomicAdd(&dig[kPvSent], (unsigned long long)keff);
-            if (dropped) atomicAdd(&dig[kPvDropped], (unsigned long long)dropped);
-        }
-        if (!init) {
-            a.own_hb[lr] += 1;
-            const unsigned long long merges = uint64_t(k) + uint64_t(uint32_t(sh.misc[5]));
-            atomicAdd(&dig[kPvRounds], 1ull);
-            atomicAdd(&dig[kPvMerges], merges);
-            atomicAdd(&dig[kPvDelivered], (unsigned long long)k);
-            if (k_all > k) atomicAdd(&dig[kPvOverflow], (unsigned long long)(k_all - k));
-            const unsigned long long j = sh.red[0][0] + sh.red[1][0] + sh.red[2][0] + sh.red[3][0];
-            const unsigned long long rm = sh.red[0][1] + sh.red[1][1] + sh.red[2][1] + sh.red[3][1];
-            const unsigned long long ev = sh.red[0][2] + sh.red[1][2] + sh.red[2][2] + sh.red[3][2];
-            if (j) atomicAdd(&dig[kPvJoins], j);
-            if (rm) atomicAdd(&dig[kPvRemoves], rm);
-            if (ev) atomicAdd(&dig[kPvEvicts], ev);
-            atomicAdd(&dig[kPvHash], sh.red[0][3] + sh.red[1][3] + sh.red[2][3] + sh.red[3][3]);
-        }
+        ulonglong2 *rec = reinterpret_cast<ulonglong2 *>(a.rowdig + (int64_t(lr) * 4 + wave) * 4);
+        rec[0] = make_ulonglong2(w0, w1);
+        if (wave == 0) rec[1].x = h;                  // w3 belongs to the send kernel
+        else rec[1] = make_ulonglong2(h, 0ull);
     }
 }
 
-template <bool kInit>
-__global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
+// kWaves: minimum waves per SIMD the register allocation must allow (8 = 8 rows per CU, the
+// LDS limit; 7 = the allocator's own choice).  A/B switch: GSP_PV_WAVES.
+template <bool kInit, int kWaves>
+__global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared sh;
-    const int32_t tid = threadIdx.x;
+    const int32_t tid = threadIdx.x, lane = tid & 63;
     const int32_t lr = blockIdx.x;
     const int32_t r = a.row0 + lr;
-    const int32_t F = a.fanout, V = a.view;
+    const int32_t V = a.view;
 
+    // the own view is requested before anything else (its latency overlaps the record's)
+    const uint64_t ent0 = (!kInit && tid < V) ? __builtin_nontemporal_load(a.prev + int64_t(lr) * V + tid)
+                                              : kPvEmpty;
     if (a.tick > a.fail_tick[r]) {          // crashed: no recv, no ops, no send
-        if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
+        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
         return;
     }
-    if (tid < F)
-        sh.peer_u[tid] = draw_u31(kDomainPeer, a.seed, uint32_t(a.tick), uint32_t(r), uint32_t(tid), 0u);
-    if (tid < 32) sh.age_hist[tid] = 0;
-    if (tid < kPvMaxInbox) sh.found[tid] = 0;
-    if (tid == 0) sh.misc[5] = 0;
 
+    PvMark pm;
+    pm.init(a.prof);
     RowOut ro{};
     int32_t k = 0, k_all = 0;
     if (kInit) {
@@ -554,60 +563,207 @@ __global__ void __launch_bounds__(kPvBlock) pview_tick_kernel(PviewTickArgs a) {
             }
             ro.len = V;
         }
-        for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.uval[i] = uint16_t(a.h0 << 5);
-        ro.ids = ids;
-        ro.vals = sh.uval;
+        for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
+        ro.ids_off = 0;
+        ro.vals_off = lds_half(sh, sh.vals);
         __syncthreads();
     } else {
-        // ---- 1. receipt order --------------------------------------------------------------
-        const int32_t o0 = a.off[lr];
-        k_all = a.off[lr + 1] - o0;
-        if (k_all > 1024) {
-            if (tid == 0) atomicOr(a.err, 1);
-            if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
+        // ---- 1. receipt record (pview_receipt_kernel), read by every wave --------------------
+        const int32_t info = a.rc_info[lr];
+        k = info & 7;
+        k_all = info >> 3;
+        if (k_all > kPvMaxSegment) {        // flagged by the receipt kernel
+            if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
             return;
         }
-        int32_t *raw = reinterpret_cast<int32_t *>(sh.keys[1]);          // scratch
-        int32_t *raw_slot = raw + 1024;
-        for (int32_t i = tid; i < k_all; i += kPvBlock) {
-            raw[i] = a.csr_src[o0 + i];
-            raw_slot[i] = a.csr_slot ? a.csr_slot[o0 + i] : raw[i] - a.row0;
+        const int32_t my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
+        const int32_t my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
+        uint32_t ssrc[kPvMaxInbox];
+        int32_t sslot[kPvMaxInbox];
+#pragma unroll
+        for (int jj = 0; jj < kPvMaxInbox; ++jj) {
+            ssrc[jj] = jj < k ? uint32_t(__builtin_amdgcn_readlane(my_src, jj)) : kNoId;
+            sslot[jj] = __builtin_amdgcn_readlane(my_slot, jj);
         }
-        __syncthreads();
-        k = k_all < a.inbox ? k_all : a.inbox;
-        for (int32_t i = tid; i < k_all; i += kPvBlock) {
-            int32_t rank = 0;
-            for (int32_t j = 0; j < k_all; ++j) rank += raw[j] < raw[i];
-            if (rank < k) {
-                sh.src[rank] = raw[i];
-                sh.slot[rank] = raw_slot[i];
+        pm.mark(0);
+        if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k <= 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else pv_merge_row<8>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        pm.mark(5);
+    }
+    pv_finish(a, sh, lr, k, k_all, kInit, ro);
+    pm.mark(6);
+    (void)0;
+}
+
+// One lane per receiver row: the K smallest senders of its CSR segment, ascending.
+__global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) {
+    const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
+    if (lr >= a.rows) return;
+    const int32_t o0 = a.off[lr], k_all = a.off[lr + 1] - o0;
+    int32_t bs[8], bl[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
+    if (k_all > kPvMaxSegment) {
+        atomicOr(a.err, 1);
+    } else {
+        for (int32_t i = 0; i < k_all; ++i) {             // insertion into the sorted best 8
+            int32_t s = a.csr_src[o0 + i];
+            int32_t sl = a.csr_slot ? a.csr_slot[o0 + i] : s - a.row0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const bool lt = s < bs[q];
+                const int32_t ts = bs[q], tl = bl[q];
+                bs[q] = lt ? s : ts;
+                bl[q] = lt ? sl : tl;
+                s = lt ? ts : s;
+                sl = lt ? tl : sl;
             }
         }
-        __syncthreads();
-        if (k == 0) pv_merge_row<1>(a, sh, lr, r, k, ro);
-        else if (k == 1) pv_merge_row<2>(a, sh, lr, r, k, ro);
-        else if (k <= 3) pv_merge_row<4>(a, sh, lr, r, k, ro);
-        else pv_merge_row<8>(a, sh, lr, r, k, ro);
     }
-    (void)V;
-    pv_finish(a, sh, lr, r, k, k_all, kInit, ro);
+    const int32_t k = k_all < a.inbox ? k_all : a.inbox;
+    int4 *ps = reinterpret_cast<int4 *>(a.rc_src + int64_t(lr) * 8);
+    int4 *pl = reinterpret_cast<int4 *>(a.rc_slot + int64_t(lr) * 8);
+    ps[0] = make_int4(bs[0], bs[1], bs[2], bs[3]);
+    ps[1] = make_int4(bs[4], bs[5], bs[6], bs[7]);
+    pl[0] = make_int4(bl[0], bl[1], bl[2], bl[3]);
+    pl[1] = make_int4(bl[4], bl[5], bl[6], bl[7]);
+    a.rc_info[lr] = (k_all > kPvMaxSegment ? 0 : k) | (k_all << 3);
+}
+
+// Peers and sends of every row (one lane per row), after the tick kernel wrote the views:
+// min(F, len) distinct members by Philox rank-select over the id order, then the drop draw.
+__global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
+    const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
+    if (lr >= a.rows) return;
+    const int32_t r = a.row0 + lr, F = a.fanout;
+    const uint32_t t = uint32_t(a.tick);
+    unsigned long long *w3 = a.rowdig + int64_t(lr) * 16 + 3;
+    bool dead = a.tick > a.fail_tick[r];
+    if (!dead && a.tick > 0) dead = (a.rc_info[lr] >> 3) > kPvMaxSegment;
+    int32_t *od = a.out_dst + int64_t(lr) * F;
+    if (dead) {
+        for (int32_t q = 0; q < F; ++q) od[q] = -1;
+        *w3 = 0ull;
+        return;
+    }
+    const int32_t len = a.len_cur[lr];
+    const int32_t keff = F < len ? F : len;
+    const uint64_t *row = a.cur + int64_t(lr) * a.view;
+    int32_t ch[16], dst[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { ch[q] = 0x7FFFFFFF; dst[q] = -1; }
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        if (kk >= keff) break;
+        const uint32_t u = draw_u31(kDomainPeer, a.seed, t, uint32_t(r), uint32_t(kk), 0u);
+        int32_t rk = int32_t(u % uint32_t(len - kk));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) rk += (q < kk && rk >= ch[q]) ? 1 : 0;   // ch ascending
+        int32_t x = rk;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {                   // insert rk, keeping ch ascending
+            const bool lt = x < ch[q];
+            const int32_t c = ch[q];
+            ch[q] = lt ? x : c;
+            x = lt ? c : x;
+        }
+        dst[kk] = int32_t(row[rk] >> 32);
+    }
+    uint32_t dropped = 0;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+        if (kk >= F) break;
+        int32_t d = dst[kk];
+        if (d >= 0) {
+            const uint32_t dr = draw_u31(kDomainSend, a.seed, t, uint32_t(r), uint32_t(d), 3u);
+            if (int32_t(dr % 100u) < a.drop_pct) { d = -1; dropped++; }
+        }
+        od[kk] = d;
+        if (d >= 0) atomicAdd(&a.deg[d], 1);
+    }
+    *w3 = uint64_t(keff) | (uint64_t(dropped) << 8);
+}
+
+// Per-tick digest: sums the per-row records (4 per row, one per wave of the tick kernel:
+// w0 = merges | delivered << 32 | round << 56, w1 = joins | removes << 16 | evicts << 32 |
+// overflow << 48, w2 = event hash, w3 = sent | dropped << 8 from the send kernel).
+__global__ void __launch_bounds__(256) pview_digest_kernel(const unsigned long long *rowdig,
+                                                           int64_t records, unsigned long long *dig) {
+    unsigned long long f[kPvFields] = {0};
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < records;
+         i += int64_t(gridDim.x) * 256) {
+        const ulonglong2 x = reinterpret_cast<const ulonglong2 *>(rowdig)[i * 2];
+        const ulonglong2 y = reinterpret_cast<const ulonglong2 *>(rowdig)[i * 2 + 1];
+        f[kPvMerges] += x.x & 0xFFFFFFFFull;
+        f[kPvDelivered] += (x.x >> 32) & 0xFFull;
+        f[kPvRounds] += (x.x >> 56) & 1ull;
+        f[kPvJoins] += x.y & 0xFFFFull;
+        f[kPvRemoves] += (x.y >> 16) & 0xFFFFull;
+        f[kPvEvicts] += (x.y >> 32) & 0xFFFFull;
+        f[kPvOverflow] += x.y >> 48;
+        f[kPvHash] += y.x;
+        f[kPvSent] += y.y & 0xFFull;
+        f[kPvDropped] += (y.y >> 8) & 0xFFull;
+    }
+    __shared__ unsigned long long part[4][kPvFields];
+    const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int q = 0; q < kPvFields; ++q) {
+        const unsigned long long s = wave_sum64(f[q]);
+        if (lane == 0) part[wave][q] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kPvFields) {
+        const int q = threadIdx.x;
+        const unsigned long long s = part[0][q] + part[1][q] + part[2][q] + part[3][q];
+        if (s) atomicAdd(&dig[(blockIdx.x % kPvDigSlots) * kPvFields + q], s);
+    }
+}
+
+bool pv_args_ok(const PviewTickArgs &a) {
+    return a.view >= 1 && a.view <= kPvMaxView && a.inbox >= 1 && a.inbox <= kPvMaxInbox &&
+           a.fanout >= 1 && a.fanout <= 16 && a.n < (1 << 21) && a.rows >= 0;
+}
+
+unsigned digest_blocks(int64_t records) {
+    return unsigned(records < 262144 ? (records + 255) / 256 : 1024);
+}
+
+void launch_send_and_digest(const PviewTickArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(pview_send_kernel, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
+    // the init tick's records hold only w3 (sends) -- its rowdig was zeroed by the host
+    const int64_t records = int64_t(a.rows) * 4;
+    hipLaunchKernelGGL(pview_digest_kernel, dim3(digest_blocks(records)), dim3(256), 0, st, a.rowdig,
+                       records, a.dig);
 }
 
 }  // namespace
 
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st) {
-    if (a.view < 1 || a.view > kPvMaxView || a.inbox < 1 || a.inbox > kPvMaxInbox ||
-        a.fanout < 1 || a.fanout > 16 || a.n >= (1 << 21))
-        return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pview_tick_kernel<true>, dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    if (!pv_args_ok(a)) return hipErrorInvalidValue;
+    if (a.rows == 0) return hipSuccess;
+    hipLaunchKernelGGL((pview_tick_kernel<true, 7>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    launch_send_and_digest(a, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st) {
+    if (a.inbox < 1 || a.inbox > kPvMaxInbox || a.rows < 0) return hipErrorInvalidValue;
+    if (a.rows == 0) return hipSuccess;
+    hipLaunchKernelGGL(pview_receipt_kernel, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
-    if (a.view < 1 || a.view > kPvMaxView || a.inbox < 1 || a.inbox > kPvMaxInbox ||
-        a.fanout < 1 || a.fanout > 16 || a.n >= (1 << 21))
-        return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pview_tick_kernel<false>, dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    if (!pv_args_ok(a)) return hipErrorInvalidValue;
+    if (a.rows == 0) return hipSuccess;
+    if (a.waves == 8)
+        hipLaunchKernelGGL((pview_tick_kernel<false, 8>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    else
+        hipLaunchKernelGGL((pview_tick_kernel<false, 7>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    launch_send_and_digest(a, st);
     return hipGetLastError();
 }
 

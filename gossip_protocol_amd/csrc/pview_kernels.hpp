@@ -5,6 +5,8 @@
 //                      Each row is sorted by id with the empty slots last (2 KB at V = 256).
 //   len[2][rows]       entries per row (by tick parity)
 //   own_hb[rows], fail_tick[n], out_dst[rows * fanout], deg/off/fill/csr_src (receiver CSR)
+//   rc_info[rows], rc_src/rc_slot[rows][8]   receipt records (K smallest senders)
+//   rowdig[rows][4][4] per-row digest records of the current tick (one per wave)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -19,6 +21,8 @@ enum : int { kPvRounds = 0, kPvMerges, kPvSent, kPvDropped, kPvDelivered, kPvOve
              kPvJoins, kPvRemoves, kPvEvicts, kPvHash, kPvFields };
 constexpr int kPvDigSlots = 256;   // spread the per-row digest atomics
 
+constexpr int kPvMaxSegment = 1024;  // messages one receiver can be sent in one tick
+
 struct PviewTickArgs {
     const uint64_t *prev;        // view table of tick t-1 (this shard's rows)
     uint64_t *cur;               // view table of tick t
@@ -29,16 +33,31 @@ struct PviewTickArgs {
     const int32_t *fail_tick;    // [n]
     int32_t *own_hb;             // [rows]
     int32_t *len_cur;            // [rows] view length of this tick
-    const int32_t *off;          // [rows + 1]
-    const int32_t *csr_src;
-    const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
+    const int32_t *rc_info;      // [rows] receipt record: k | k_all << 3
+    const int32_t *rc_src;       // [rows][8] the k smallest senders, ascending
+    const int32_t *rc_slot;      // [rows][8] their rows: >= 0 local, < 0 remote (-slot - 1)
     int32_t *out_dst;            // [rows * fanout]
     int32_t *deg;                // [n]
+    unsigned long long *rowdig;  // [rows][4][4] per-row digest records of this tick
     unsigned long long *dig;     // [kPvDigSlots][kPvFields] of this tick
+    int32_t *err;
+    unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
+    int32_t waves;               // register budget variant of the tick kernel (7 or 8)
+};
+constexpr int kPvProfPhases = 10;
+
+struct PviewReceiptArgs {
+    const int32_t *off;          // [rows + 1] receiver CSR
+    const int32_t *csr_src;      // sender ids
+    const int32_t *csr_slot;     // row mode: sender rows (null: local row = src - row0)
+    int32_t rows, row0, inbox;
+    int32_t *rc_info, *rc_src, *rc_slot;
     int32_t *err;
 };
 
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st);
+hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st);
+// tick kernel, then the send kernel (peers, drops) and the digest reduction
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st);
 
 }  // namespace gsp
