@@ -106,10 +106,10 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     p0 = eng.perf()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     eng.step(steps)
-    torch.cuda.synchronize()
+    _sync()
     if dist is not None:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -130,10 +130,10 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     xgmi = (p1["xgmi_bytes"] - p0["xgmi_bytes"]) / steps
     eng.close()
     if dist is not None:
-        t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device=_dev())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         u = torch.tensor([rounds, merges, bytes_per_launch, xgmi], dtype=torch.float64,
-                         device="cuda")
+                         device=_dev())
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         el, kern_ms, xch_ms = (x.item() for x in t)
         rounds, merges, bytes_per_launch, xgmi = (x.item() for x in u)
@@ -160,7 +160,104 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     return out
 
 
-def main():
+def run_full(nodes, steps, warmup, world, local, dist):
+    """Full-view workload (config 3 rules) on `world` GPUs: one GPU fused, or column shards.
+    Returns job totals (time and kernel time are the slowest rank's)."""
+    import torch
+    from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
+    kw = dict(fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM,
+              seed=SEED, max_ticks=warmup + steps)
+    if dist is not None:
+        from gossip_protocol_amd.dist import make_rank_engine
+        eng = make_rank_engine(nodes, local, **kw)
+    else:
+        eng = ScaleEngine(nodes, device=local, **kw)
+    eng.step(warmup)
+    eng.sync()
+    perf0 = eng.perf()
+    if dist is not None:
+        dist.barrier()
+    _sync()
+    t0 = time.perf_counter()
+    eng.step(steps)
+    _sync()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    eng.sync()
+    perf1 = eng.perf()
+    xgmi_tick = (perf1["xgmi_bytes"] - perf0["xgmi_bytes"]) / steps
+    rounds = merges = delivered = 0
+    for t in range(warmup + 1, warmup + steps + 1):
+        d = eng.digest(t)
+        rounds += d["node_rounds"]
+        merges += d["merges"]
+        delivered += d["delivered"]
+    stride = eng.layout()[2]
+    launches = max(perf1["merge_launches"] - perf0["merge_launches"], 1)
+    kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / launches
+    csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / launches
+    eng.close()
+    if dist is not None:
+        # per-row counts live on rank 0 only (sum = job total); the step and kernel times are
+        # the slowest rank's (max); every rank sends its own exchange bytes (sum)
+        u = torch.tensor([rounds, merges, delivered, xgmi_tick], dtype=torch.float64,
+                         device=_dev())
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        rounds, merges, delivered, xgmi_tick = (x.item() for x in u)
+        m = torch.tensor([el, kern_ms, csr_ms], dtype=torch.float64, device=_dev())
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        el, kern_ms, csr_ms = (x.item() for x in m)
+    # algorithmic bytes per launch: own row read + write and one sender row per message
+    # (2-byte entries), one 4-byte CSR entry per message; every shard streams its slice
+    # (stride columns) of each such row, so the job moves `world` slices
+    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * world / steps
+    return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
+            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick}
+
+
+def summarize_full(r, nodes, steps, world):
+    achieved = r["bytes_per_launch"] / (r["kern_ms"] * 1e-3) / 1e9     # summed over ranks
+    peak = PEAK_HBM_GBS * world
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if nodes == N_NODES and world == 1 and os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    cfg = "config3" if nodes == N_NODES else "config4" if nodes == 262144 else "full view"
+    return {
+        "metric": "gossip node-rounds/sec (+ merge-kernel HBM GB/s, % peak)",
+        "value": r["rounds"] / r["el"], "unit": "node-rounds/s",
+        "ms_per_step": r["el"] * 1e3 / steps, "scaling": "strong", "dtype": "u16",
+        "data": "synthetic (pre-joined full-view membership, Philox peers/failures)",
+        "config": {"workload": "%s: %d nodes full view, fanout %d, 1%% random crash at t=%d, "
+                               "no drops" % (cfg, nodes, FANOUT, FAIL_TICK),
+                   "nodes": nodes, "view": nodes, "fanout": FANOUT, "entry_bytes": 2,
+                   "parallelism": "columns%d" % world if world > 1 else "1gpu"},
+        "merges_per_s": r["merges"] / r["el"],
+        "xgmi_bytes_per_tick": r["xgmi_tick"],
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
+                     "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
+                     "kernel_ms": r["kern_ms"], "csr_ms": r["csr_ms"],
+                     "algorithmic_bytes_per_launch": r["bytes_per_launch"]},
+    }
+
+
+def _sync():
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def _dev():
+    """Device of the timing reductions: the GPU (RCCL) or, for the gloo CPU tests, the host."""
+    import torch
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
@@ -169,7 +266,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pview", action="store_true", help="skip the config-5 line item")
     ap.add_argument("--pview-nodes", type=int, default=PV_NODES)
-    args = ap.parse_args()
+    ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item (N > 1)")
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -178,123 +276,31 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
-
-    if world > 1:
-        # column shards: the same config-3 workload split N ways (strong scaling)
-        from gossip_protocol_amd.dist import make_rank_engine
-        eng = make_rank_engine(args.nodes, local, fanout=FANOUT, fail_mode=FAIL_RANDOM,
-                               fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM, seed=SEED,
-                               max_ticks=args.warmup + args.steps)
-    else:
-        eng = ScaleEngine(args.nodes, fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK,
-                          fail_ppm=FAIL_PPM, seed=SEED, max_ticks=args.warmup + args.steps,
-                          device=local)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    eng.step(args.warmup)
-    eng.sync()
-    perf0 = eng.perf()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng.step(args.steps)
-    torch.cuda.synchronize()
-    barrier()
-    el = time.perf_counter() - t0
-    eng.sync()
-    perf1 = eng.perf()
-    xgmi_tick = (perf1["xgmi_bytes"] - perf0["xgmi_bytes"]) / args.steps
-
-    rounds = merges = delivered = 0
-    for t in range(args.warmup + 1, args.warmup + args.steps + 1):
-        d = eng.digest(t)
-        rounds += d["node_rounds"]
-        merges += d["merges"]
-        delivered += d["delivered"]
-    if dist is not None:
-        # every rank streams its slice of every processed row and of every sender row
-        tot = torch.tensor([rounds, delivered], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        rows_all, delivered_all = tot[0].item(), tot[1].item()
-    else:
-        rows_all, delivered_all = rounds, delivered
-    stride = eng.layout()[2]
-    launches = perf1["merge_launches"] - perf0["merge_launches"]
-    kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / max(launches, 1)
-    csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / max(launches, 1)
-    # algorithmic bytes per launch: own row read + write, one sender row per message
-    # (2-byte entries), one 4-byte CSR entry per message
-    # per shard: its slice (stride columns) of every processed and every sender row; the
-    # job moves `world` slices (row counts are kept by rank 0 only, so rows_all = job total)
-    bytes_per_launch = ((2.0 * rows_all + delivered_all) * stride * 2.0 +
-                        delivered_all * 4.0) * world / args.steps
-
-    if dist is not None:
-        # per-row counts live on rank 0 only (sum = job total); each rank moves its own
-        # slice's bytes (sum); the step time and kernel time are the slowest rank's (max)
-        t = torch.tensor([el, rounds, merges, bytes_per_launch, kern_ms], dtype=torch.float64,
-                         device="cuda")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        el = tmax[0].item()
-        rounds, merges = tsum[1].item(), tsum[2].item()
-        kern_ms = tmax[4].item()
-        x = torch.tensor([xgmi_tick], dtype=torch.float64, device="cuda")
-        dist.all_reduce(x, op=dist.ReduceOp.SUM)
-        xgmi_tick = x.item()
-    eng.close()
+        if not dist.is_initialized():
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
+    full = run_full(args.nodes, args.steps, args.warmup, world, local, dist)
     pv = None
     if not args.no_pview:
         pv = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
                        not args.no_cpu_baseline)
+    f262 = None
+    if world > 1 and not args.no_262k:
+        # BASELINE config 4: 262,144 nodes full view over the same column shards (its 137 GB
+        # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)
+        r = run_full(262144, min(args.steps, 8), 2, world, local, dist)
+        f262 = summarize_full(r, 262144, min(args.steps, 8), world)
 
     if rank == 0:
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9     # summed over ranks
-        peak = PEAK_HBM_GBS * world
-        traffic = None
-        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(prof):
-            try:
-                traffic = json.load(open(prof)).get("bytes_per_launch")
-            except Exception:
-                traffic = None
-        out = {
-            "metric": "gossip node-rounds/sec (+ merge-kernel HBM GB/s, % peak)",
-            "value": rounds / el,
-            "unit": "node-rounds/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el * 1e3 / args.steps,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "u16",
-            "data": "synthetic (pre-joined full-view membership, Philox peers/failures)",
-            "config": {"workload": "config3: %d nodes full view, fanout %d, 1%% random crash at "
-                                   "t=%d, no drops" % (args.nodes, FANOUT, FAIL_TICK),
-                       "nodes": args.nodes, "view": args.nodes, "fanout": FANOUT,
-                       "entry_bytes": 2,
-                       "parallelism": "columns%d" % world if world > 1 else "1gpu"},
-            "merges_per_s": merges / el,
-            "xgmi_bytes_per_tick": xgmi_tick,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak,
-                         "unit": "GB/s", "frac": achieved / peak, "traffic": traffic,
-                         "kernel": "scale_tick_kernel", "kernel_ms": kern_ms,
-                         "csr_ms": csr_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
-        }
+        out = summarize_full(full, args.nodes, args.steps, world)
+        out.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                    "higher_is_better": True, "vs_baseline": None})
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         if pv is not None:
             out["pview"] = pv
+        if f262 is not None:
+            out["full262k"] = f262
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -9,33 +9,61 @@ namespace {
 
 constexpr int kMaxFanout = 16;
 
+__device__ inline uint32_t wave_excl_scan(uint32_t v, uint32_t *total) {
+    const int32_t lane = threadIdx.x & 63;
+    uint32_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += u;
+    }
+    *total = __shfl(incl, 63, 64);
+    return incl - v;
+}
+
+// One lane per local sender; slots in pair / record regions are claimed with one atomic per
+// (wave, destination shard), not one per message.
 __global__ void __launch_bounds__(256) rowx_pack_kernel(RowxArgs a) {
     const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
-    if (lr >= a.rows) return;
+    const bool live = lr < a.rows;
     const int32_t F = a.fanout;
-    int32_t h_of[kMaxFanout], p_of[kMaxFanout];
+    int32_t h_of[kMaxFanout], d_of[kMaxFanout];
 #pragma unroll
     for (int k = 0; k < kMaxFanout; ++k) {
         h_of[k] = -1;
-        p_of[k] = -1;
-        if (k >= F) continue;
+        d_of[k] = -1;
+        if (!live || k >= F) continue;
         const int32_t d = a.out_dst[int64_t(lr) * F + k];
         if (d < 0) continue;
         const int32_t h = rowx_owner(d, a.n, a.shards);
         if (h == a.shard) continue;                   // delivered by the local scatter
         h_of[k] = h;
-        int32_t p = -1;
+        d_of[k] = d;
+    }
+    const int32_t lane = threadIdx.x & 63;
+    for (int32_t h = 0; h < a.shards; ++h) {          // wave-uniform loop
+        uint32_t nm = 0;
 #pragma unroll
-        for (int q = 0; q < kMaxFanout; ++q)          // sender row already bound for h?
-            if (q < k && h_of[q] == h) p = p_of[q];
-        if (p < 0) {
-            p = atomicAdd(&a.pair_cnt[h], 1);
-            a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
+        for (int k = 0; k < kMaxFanout; ++k) nm += h_of[k] == h ? 1u : 0u;
+        const unsigned long long pm = __ballot(nm > 0);
+        if (!pm) continue;
+        uint32_t mtot = 0;
+        const uint32_t mpre = wave_excl_scan(nm, &mtot);
+        int32_t pbase = 0, mbase = 0;
+        if (lane == 0) {
+            pbase = atomicAdd(&a.pair_cnt[h], int32_t(__popcll(pm)));
+            mbase = atomicAdd(&a.msg_cnt[h], int32_t(mtot));
         }
-        p_of[k] = p;
-        const int32_t m = atomicAdd(&a.msg_cnt[h], 1);
-        a.send_rec[int64_t(h) * a.msg_cap + m] =
-            RowxRec{a.row0 + lr, d - rowx_row0(h, a.n, a.shards), p};
+        pbase = __shfl(pbase, 0, 64);
+        mbase = __shfl(mbase, 0, 64);
+        if (!nm) continue;
+        const int32_t p = pbase + int32_t(__popcll(pm & ((1ull << lane) - 1ull)));
+        a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
+        int32_t m = mbase + int32_t(mpre);
+        const int32_t hrow0 = rowx_row0(h, a.n, a.shards);
+#pragma unroll
+        for (int k = 0; k < kMaxFanout; ++k)
+            if (h_of[k] == h) a.send_rec[int64_t(h) * a.msg_cap + m++] = RowxRec{a.row0 + lr, d_of[k] - hrow0, p};
     }
 }
 

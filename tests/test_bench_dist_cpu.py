@@ -1,0 +1,103 @@
+"""bench.py's N > 1 path on CPU: two gloo ranks run bench.main() over stand-in engines.
+
+The engines are replaced by deterministic fakes (the real ones need a GPU), so what runs is
+bench.py's own multi-rank logic: barriers around the timed region, the max-over-ranks time
+and kernel time, the job-total node-rounds / bytes / xGMI reductions, the three line items
+(config 3 headline, config 5 `pview`, config 4 `full262k`) and the single rank-0 JSON line.
+"""
+import io
+import json
+import os
+import socket
+import contextlib
+
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N_STEPS, N_WARM = 3, 1
+
+
+class FakeEngine:
+    """Per-tick digest: `rows` node-rounds on rank 0 (column shards count rows on shard 0),
+    2 deliveries per round; kernel 2 ms (rank 0) / 3 ms (rank 1) per tick."""
+
+    def __init__(self, n, rank, world, pview=False):
+        self.n, self.rank, self.world, self.pview = n, rank, world, pview
+        self.t = 0
+
+    def step(self, k):
+        self.t += k
+
+    def sync(self):
+        pass
+
+    def perf(self):
+        ms = 2.0 + self.rank
+        return {"merge_launches": self.t, "merge_ms": ms * self.t, "csr_ms": 0.5 * self.t,
+                "xgmi_bytes": 1000.0 * (self.rank + 1) * self.t}
+
+    def digest(self, t):
+        if self.pview:                               # row shards: every rank counts its rows
+            rows = self.n // self.world
+        else:
+            rows = self.n if self.rank == 0 else 0
+        return {"tick": t, "node_rounds": rows, "merges": 3 * rows, "delivered": 2 * rows,
+                "overflow": 0}
+
+    def layout(self):
+        return (self.world, self.rank, self.n // self.world)
+
+    def close(self):
+        pass
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gossip_protocol_amd.dist as gd
+    gd.make_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world)
+    gd.make_pview_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world, pview=True)
+    import bench
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--steps", str(N_STEPS), "--warmup", str(N_WARM), "--nodes", "1024",
+                    "--pview-nodes", "4096", "--no-cpu-baseline"])
+    q.put((rank, buf.getvalue()))
+
+
+def test_bench_two_ranks_gloo():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    outs = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert outs[1].strip() == ""                      # only rank 0 prints
+    lines = [l for l in outs[0].splitlines() if l.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == N_STEPS and d["warmup"] == N_WARM
+    assert d["config"]["parallelism"] == "columns2"
+    rf = d["roofline"]
+    assert rf["kernel_ms"] == 3.0                     # slowest rank
+    assert rf["peak"] == 16000.0
+    # job bytes per launch: (2 rows + 2 rows delivered) * stride(512) * 2 B + CSR, x 2 slices
+    assert rf["algorithmic_bytes_per_launch"] == ((2 * 1024 + 2 * 1024) * 512 * 2 + 2 * 1024 * 4) * 2
+    assert abs(d["value"] - 1024 * N_STEPS / (d["ms_per_step"] * N_STEPS / 1e3)) < 1e-6 * d["value"]
+    assert d["xgmi_bytes_per_tick"] == 3000.0         # sum over ranks
+    pv = d["pview"]
+    assert pv["config"]["parallelism"] == "rows2"
+    assert pv["xgmi_bytes_per_tick"] == 3000.0
+    assert pv["roofline"]["kernel_ms"] == 3.0
+    assert abs(pv["value"] - 4096 * min(N_STEPS, 30) / (pv["ms_per_step"] * min(N_STEPS, 30) / 1e3)) \
+        < 1e-6 * pv["value"]
+    f = d["full262k"]
+    assert f["config"]["nodes"] == 262144 and f["config"]["workload"].startswith("config4")
