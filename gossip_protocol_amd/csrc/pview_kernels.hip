@@ -344,11 +344,25 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     // ---- 5a. survivors (and adopted orphans), compacted in id order -------------------------
     // for_each visits this lane's survivors in id order as (value, id)
     const uint32_t fresh = (1u << 5) | t5;                     // an orphan: (hb 1, ts t)
-    auto for_each = [&](auto &&f) {
-        if (!adopt) {
+    // Almost every sender is an orphan (views are tiny next to n), but a lane brackets more
+    // than one only rarely: one orphan per lane takes the short path, a wave with any lane
+    // holding two or more takes the general one.
+    const int32_t n_orph = __popc(adopt);
+    uint32_t o_x = 0;
+    int32_t o_p = -1;
+    if (n_orph == 1) {
 #pragma unroll
-            for (int e = 0; e < Q; ++e)
-                if (res[e]) f(res[e], rid[e]);
+        for (int jj = 0; jj < kPvMaxInbox; ++jj)
+            if ((adopt >> jj) & 1u) { o_x = ssrc[jj]; o_p = ains[jj]; }
+    }
+    const bool multi = __ballot(n_orph > 1) != 0ull;          // wave-uniform
+    auto for_each = [&](auto &&f) {
+        if (!multi) {
+#pragma unroll
+            for (int e = 0; e <= Q; ++e) {
+                if (o_p == e) f(fresh, o_x);
+                if (e < Q && res[e]) f(res[e], rid[e]);
+            }
         } else {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
@@ -429,18 +443,19 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             }
             const unsigned long long hit = __ballot(incl >= need);
             const int32_t lb = __builtin_ffsll(hit) - 1;
-            uint32_t hs = 0, n2 = 0;
-            if (lane == lb) {
-                uint32_t cum = incl - loc;
-                for (int b = 0; b < 32; ++b) {
-                    const int32_t h = 2047 - 32 * lane - b;
-                    const uint32_t c = h16[h];
-                    if (cum + c >= need) { hs = uint32_t(h); n2 = need - cum; break; }
-                    cum += c;
-                }
+            // lanes 0..31 take the boundary lane's 32 bins (descending hb) and scan them
+            const uint32_t before = __shfl(incl - loc, lb, 64);
+            const uint32_t c = lane < 32 ? uint32_t(h16[2047 - 32 * lb - lane]) : 0u;
+            uint32_t ci = c;
+#pragma unroll
+            for (int d = 1; d < 32; d <<= 1) {
+                const uint32_t u = __shfl_up(ci, d, 64);
+                if (lane >= d) ci += u;
             }
-            hstar = __shfl(hs, lb, 64);
-            need2 = __shfl(n2, lb, 64);                        // kept among (astar, hstar) ties
+            const unsigned long long hit2 = __ballot(lane < 32 && before + ci >= need);
+            const int32_t lh = __builtin_ffsll(hit2) - 1;
+            hstar = uint32_t(2047 - 32 * lb - lh);
+            need2 = need - before - (__shfl(ci, lh, 64) - __shfl(c, lh, 64));  // kept among ties
         }
         pm.mark(8);
         // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
