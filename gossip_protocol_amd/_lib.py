@@ -121,6 +121,11 @@ SIGNATURES = {
                                              ctypes.c_void_p, P(ctypes.c_void_p)]),
     "gsp_scale_create_group": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
                                               P(ctypes.c_void_p)]),
+    "gsp_scale_create_rank_layout": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
+                                                    c_int32, ctypes.c_void_p, c_int32,
+                                                    P(ctypes.c_void_p)]),
+    "gsp_scale_create_group_layout": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
+                                                     c_int32, P(ctypes.c_void_p)]),
     "gsp_scale_layout": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), P(c_int64)]),
     "gsp_scale_hip_stream": (ctypes.c_int, [ctypes.c_void_p, P(ctypes.c_void_p)]),
     "gsp_pview_create": (ctypes.c_int, [P(GspPviewParams), ctypes.c_int, P(ctypes.c_void_p)]),

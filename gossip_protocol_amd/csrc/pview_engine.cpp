@@ -25,6 +25,7 @@
 #include "common.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
+#include "rowx_host.hpp"
 #include "rowx_kernels.hpp"
 #include "scale_kernels.hpp"
 
@@ -37,24 +38,17 @@ namespace {
 struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
-    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, csr_slot,
-        err, tile_sum, rc_info, rc_src, rc_slot;
+    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
+        tile_sum, rc_info, rc_src, rc_slot;
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
-    // row exchange (G > 1)
-    gsp::DevBuf<int32_t> cnt, cnt_all, recv_msgs, pair_row;
-    gsp::DevBuf<uint64_t> send_rows, recv_rows;
-    gsp::DevBuf<gsp::RowxRec> send_rec, recv_rec;
+    gsp::RowxBufs x;             // row exchange (G > 1)
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
-        for (auto *x : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &csr_slot,
-                        &err, &tile_sum, &cnt, &cnt_all, &recv_msgs, &pair_row, &rc_info, &rc_src,
-                        &rc_slot})
-            x->release();
-        send_rows.release();
-        recv_rows.release();
-        send_rec.release();
-        recv_rec.release();
+        for (auto *b : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &err,
+                        &tile_sum, &rc_info, &rc_src, &rc_slot})
+            b->release();
+        x.release();
         dig.release();
         prof.release();
         rowdig.release();
@@ -99,7 +93,7 @@ struct gsp_pview {
         gsp::PviewTickArgs a{};
         a.prev = sh.table[(t + 1) & 1].p;
         a.cur = sh.table[t & 1].p;
-        a.remote = rowmode ? sh.recv_rows.p : nullptr;
+        a.remote = rowmode ? sh.x.recv_rows.p : nullptr;
         a.n = p.n;
         a.view = p.view;
         a.inbox = p.inbox;
@@ -131,7 +125,7 @@ struct gsp_pview {
         gsp::PviewReceiptArgs a{};
         a.off = sh.off.p;
         a.csr_src = sh.csr_src.p;
-        a.csr_slot = rowmode ? sh.csr_slot.p : nullptr;
+        a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
         a.rows = sh.rows;
         a.row0 = sh.row0;
         a.inbox = p.inbox;
@@ -140,27 +134,6 @@ struct gsp_pview {
         a.rc_slot = sh.rc_slot.p;
         a.err = sh.err.p;
         return a;
-    }
-
-    gsp::RowxArgs rowx(PvShard &sh, int32_t t_sent) const {
-        gsp::RowxArgs x{};
-        x.n = p.n;
-        x.shards = shards;
-        x.shard = sh.g;
-        x.fanout = p.fanout;
-        x.row0 = sh.row0;
-        x.rows = sh.rows;
-        x.pair_cap = pair_cap;
-        x.msg_cap = msg_cap;
-        x.row_words = p.view;
-        x.out_dst = sh.out_dst.p;
-        x.table = sh.table[t_sent & 1].p;
-        x.pair_cnt = sh.cnt.p;
-        x.msg_cnt = sh.cnt.p + shards;
-        x.pair_row = sh.pair_row.p;
-        x.send_rows = sh.send_rows.p;
-        x.send_rec = sh.send_rec.p;
-        return x;
     }
 
     PvShard *holder(int32_t r) {
@@ -214,19 +187,8 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     GSP_HIP(sh.rc_slot.alloc(rows * 8));
     GSP_HIP(sh.rowdig.alloc(rows * 16));
     GSP_HIP(hipMemsetAsync(sh.rowdig.p, 0, rows * 16 * 8, st));
-    if (s->rowmode) {
-        const size_t G2 = size_t(G);
-        GSP_HIP(sh.csr_slot.alloc(size_t(n) * F));
-        GSP_HIP(sh.cnt.alloc(2 * G2));
-        GSP_HIP(sh.cnt_all.alloc(2 * G2 * G2));
-        GSP_HIP(sh.recv_msgs.alloc(G2));
-        GSP_HIP(sh.pair_row.alloc(G2 * size_t(s->pair_cap)));
-        GSP_HIP(sh.send_rows.alloc(G2 * size_t(s->pair_cap) * size_t(V)));
-        GSP_HIP(sh.recv_rows.alloc(G2 * size_t(s->pair_cap) * size_t(V)));
-        GSP_HIP(sh.send_rec.alloc(G2 * size_t(s->msg_cap)));
-        GSP_HIP(sh.recv_rec.alloc(G2 * size_t(s->msg_cap)));
-        GSP_HIP(hipMemsetAsync(sh.recv_msgs.p, 0, G2 * 4, st));
-    }
+    if (s->rowmode)
+        GSP_HIP(sh.x.alloc(G, s->pair_cap, s->msg_cap, V, int64_t(n) * F, st));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
@@ -242,86 +204,15 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
 }
 
 // Move the sender views of tick t_sent's cross-shard messages to their destination shards and
-// build every local shard's receiver CSR for tick t_sent + 1.
+// build every local shard's receiver CSR for tick t_sent + 1 (rowx_host.cpp).
 int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
-    const int32_t G = s->shards, V = s->p.view, F = s->p.fanout;
-    hipStream_t st = s->st;
-    for (PvShard &sh : s->local) {
-        GSP_HIP(hipMemsetAsync(sh.cnt.p, 0, size_t(2 * G) * 4, st));
-        const gsp::RowxArgs x = s->rowx(sh, t_sent);
-        GSP_HIP(gsp::launch_rowx_pack(x, st));
-        GSP_HIP(gsp::launch_rowx_gather(x, st));
-    }
-    // counts of every shard -> cnt_all[G][2G] (first local shard's copy is read by the host)
-    if (s->comm) {
-        PvShard &sh = s->local[0];
-        GSP_NCCL(ncclAllGather(sh.cnt.p, sh.cnt_all.p, size_t(2 * G), ncclInt32, s->comm, st));
-    } else {
-        for (PvShard &src : s->local)
-            GSP_HIP(hipMemcpyAsync(s->local[0].cnt_all.p + size_t(src.g) * 2 * G, src.cnt.p,
-                                   size_t(2 * G) * 4, hipMemcpyDeviceToDevice, st));
-    }
-    GSP_HIP(hipMemcpyAsync(s->h_cnt, s->local[0].cnt_all.p, size_t(2 * G) * G * 4,
-                           hipMemcpyDeviceToHost, st));
-    GSP_HIP(hipStreamSynchronize(st));
-    auto pairs = [&](int32_t g, int32_t h) { return int64_t(s->h_cnt[size_t(g) * 2 * G + h]); };
-    auto msgs = [&](int32_t g, int32_t h) { return int64_t(s->h_cnt[size_t(g) * 2 * G + G + h]); };
-    const size_t row_bytes = size_t(V) * 8, rec_bytes = sizeof(gsp::RowxRec);
-    double bytes = 0;
-    if (s->comm) {
-        PvShard &sh = s->local[0];
-        const int32_t me = sh.g;
-        GSP_NCCL(ncclGroupStart());
-        for (int32_t h = 0; h < G; ++h) {
-            if (h == me) continue;
-            const size_t so = size_t(h) * size_t(s->pair_cap), mo = size_t(h) * size_t(s->msg_cap);
-            if (pairs(me, h))
-                GSP_NCCL(ncclSend(sh.send_rows.p + so * V, size_t(pairs(me, h)) * V, ncclUint64, h,
-                                  s->comm, st));
-            if (msgs(me, h))
-                GSP_NCCL(ncclSend(sh.send_rec.p + mo, size_t(msgs(me, h)) * 3, ncclInt32, h, s->comm, st));
-            if (pairs(h, me))
-                GSP_NCCL(ncclRecv(sh.recv_rows.p + so * V, size_t(pairs(h, me)) * V, ncclUint64, h,
-                                  s->comm, st));
-            if (msgs(h, me))
-                GSP_NCCL(ncclRecv(sh.recv_rec.p + mo, size_t(msgs(h, me)) * 3, ncclInt32, h, s->comm, st));
-            bytes += double(pairs(me, h)) * row_bytes + double(msgs(me, h)) * rec_bytes;
-        }
-        GSP_NCCL(ncclGroupEnd());
-    } else {
-        for (PvShard &src : s->local)
-            for (PvShard &dst : s->local) {
-                const int32_t g = src.g, h = dst.g;
-                if (g == h) continue;
-                const size_t so = size_t(h) * size_t(s->pair_cap), mo = size_t(h) * size_t(s->msg_cap);
-                const size_t ro = size_t(g) * size_t(s->pair_cap), qo = size_t(g) * size_t(s->msg_cap);
-                if (pairs(g, h))
-                    GSP_HIP(hipMemcpyAsync(dst.recv_rows.p + ro * V, src.send_rows.p + so * V,
-                                           size_t(pairs(g, h)) * row_bytes, hipMemcpyDeviceToDevice, st));
-                if (msgs(g, h))
-                    GSP_HIP(hipMemcpyAsync(dst.recv_rec.p + qo, src.send_rec.p + mo,
-                                           size_t(msgs(g, h)) * rec_bytes, hipMemcpyDeviceToDevice, st));
-                bytes += double(pairs(g, h)) * row_bytes + double(msgs(g, h)) * rec_bytes;
-            }
-    }
-    s->perf.xgmi_bytes += bytes;
-    for (size_t i = 0; i < s->local.size(); ++i) {
-        PvShard &sh = s->local[i];
-        int32_t *hr = s->h_recv + i * size_t(G);
-        for (int32_t h = 0; h < G; ++h) hr[h] = h == sh.g ? 0 : int32_t(msgs(h, sh.g));
-        GSP_HIP(hipMemcpyAsync(sh.recv_msgs.p, hr, size_t(G) * 4, hipMemcpyHostToDevice, st));
-        GSP_HIP(gsp::launch_rowx_recv_deg(sh.recv_rec.p, sh.recv_msgs.p, G, s->msg_cap, sh.row0,
-                                          sh.deg.p, st));
-        GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p + sh.row0, sh.off.p, sh.rows, sh.tile_sum.p, st));
-        GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(sh.rows) * 4, st));
-        GSP_HIP(gsp::launch_rowx_scatter_local(sh.out_dst.p, sh.rows, F, sh.row0, sh.off.p, sh.fill.p,
-                                               sh.csr_src.p, sh.csr_slot.p, st));
-        GSP_HIP(gsp::launch_rowx_scatter_remote(sh.recv_rec.p, sh.recv_msgs.p, G, s->msg_cap,
-                                                s->pair_cap, sh.off.p, sh.fill.p, sh.csr_src.p,
-                                                sh.csr_slot.p, st));
-        GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(s->p.n) * 4, st));
-    }
-    return GSP_OK;
+    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, s->p.view, s->pair_cap, s->msg_cap,
+                     s->comm, s->st, s->h_cnt, s->h_recv};
+    std::vector<gsp::RowxShard> v;
+    for (PvShard &sh : s->local)
+        v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p, sh.table[t_sent & 1].p,
+                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p, &sh.x});
+    return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
 }
 
 int pview_collect(gsp_pview *s) {

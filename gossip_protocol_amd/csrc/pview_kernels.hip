@@ -671,7 +671,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     for (int q = 0; q < 16; ++q) { ch[q] = 0x7FFFFFFF; dst[q] = -1; }
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-        if (kk >= keff) break;
+        if (kk >= keff) continue;
         const uint32_t u = draw_u31(kDomainPeer, a.seed, t, uint32_t(r), uint32_t(kk), 0u);
         int32_t rk = int32_t(u % uint32_t(len - kk));
 #pragma unroll
@@ -689,7 +689,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     uint32_t dropped = 0;
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
-        if (kk >= F) break;
+        if (kk >= F) continue;
         int32_t d = dst[kk];
         if (d >= 0) {
             const uint32_t dr = draw_u31(kDomainSend, a.seed, t, uint32_t(r), uint32_t(d), 3u);

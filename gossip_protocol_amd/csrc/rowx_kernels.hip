@@ -57,13 +57,19 @@ __global__ void __launch_bounds__(256) rowx_pack_kernel(RowxArgs a) {
         pbase = __shfl(pbase, 0, 64);
         mbase = __shfl(mbase, 0, 64);
         if (!nm) continue;
+        // counts keep growing past the capacity (the host sees them and fails the tick);
+        // nothing is written out of bounds
         const int32_t p = pbase + int32_t(__popcll(pm & ((1ull << lane) - 1ull)));
-        a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
+        if (p < a.pair_cap) a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
         int32_t m = mbase + int32_t(mpre);
         const int32_t hrow0 = rowx_row0(h, a.n, a.shards);
 #pragma unroll
         for (int k = 0; k < kMaxFanout; ++k)
-            if (h_of[k] == h) a.send_rec[int64_t(h) * a.msg_cap + m++] = RowxRec{a.row0 + lr, d_of[k] - hrow0, p};
+            if (h_of[k] == h) {
+                if (m < a.msg_cap && p < a.pair_cap)
+                    a.send_rec[int64_t(h) * a.msg_cap + m] = RowxRec{a.row0 + lr, d_of[k] - hrow0, p};
+                m++;
+            }
     }
 }
 
@@ -74,7 +80,7 @@ __global__ void __launch_bounds__(256) rowx_gather_kernel(RowxArgs a) {
     const int64_t nw = (int64_t(gridDim.x) * 256) >> 6;
     const int32_t W = a.row_words;
     for (int32_t h = 0; h < a.shards; ++h) {
-        const int64_t cnt = a.pair_cnt[h];
+        const int64_t cnt = a.pair_cnt[h] < a.pair_cap ? a.pair_cnt[h] : a.pair_cap;
         for (int64_t p = w0; p < cnt; p += nw) {
             const int32_t lr = a.pair_row[int64_t(h) * a.pair_cap + p];
             const uint64_t *src = a.table + int64_t(lr) * W;

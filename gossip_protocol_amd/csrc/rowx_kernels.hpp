@@ -12,8 +12,10 @@
 //   csr      receiver CSR over the local rows: local messages (csr_slot = local row) and
 //            received records (csr_slot = -(h * pair_cap + pair) - 1 into the remote rows).
 // HBM layout per shard: send_rows[G][pair_cap][row_words], send_rec[G][msg_cap],
-// recv_rows[G][pair_cap][row_words], recv_rec[G][msg_cap]; pair_cap = max rows of a shard,
-// msg_cap = pair_cap * fanout.
+// recv_rows[G][pair_cap][row_words], recv_rec[G][msg_cap].  pair_cap = max rows of a shard
+// makes every tick fit (a sender row goes to a shard at most once); an engine may size it
+// smaller for large rows, in which case a count above the capacity fails the tick
+// (GSP_ERR_CAPACITY) and nothing is written out of bounds.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>

@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -21,6 +22,7 @@
 
 #include "common.hpp"
 #include "philox.hpp"
+#include "rowx_host.hpp"
 #include "scale_kernels.hpp"
 
 namespace {
@@ -28,6 +30,8 @@ namespace {
 struct Shard {
     int32_t g = 0;
     int32_t col0 = 0;
+    int32_t row0 = 0, rows = 0;    // row layout: rows [row0, row0 + rows); else all n rows
+    gsp::RowxBufs x;               // row layout exchange buffers
     gsp::DevBuf<uint16_t> table[2];
     gsp::DevBuf<int32_t> own_hb, fail_tick, cnt_total[2], cnt_slice, cnt_all, out_dst, picks,
         deg, off, fill, csr_src, err, tile_sum;
@@ -41,6 +45,7 @@ struct Shard {
             x->release();
         bitmap.release();
         dig.release();
+        x.release();
     }
 };
 
@@ -52,7 +57,10 @@ struct gsp_scale {
     hipStream_t st = nullptr;
     int32_t shards = 1;        // G: column shards in the whole job
     int32_t rank = 0;          // first shard index held by this engine
-    bool sliced = false;       // column mode (G > 1)
+    bool sliced = false;       // column layout (G > 1)
+    bool rowmode = false;      // row layout (G > 1): sender rows move between shards
+    int64_t pair_cap = 0, msg_cap = 0;
+    int32_t *h_cnt = nullptr, *h_recv = nullptr;   // pinned exchange counts (row layout)
     ncclComm_t comm = nullptr; // one shard per process when set
     int64_t width = 0;         // n rounded up to 2048 * G
     int64_t stride = 0;        // columns per shard
@@ -82,12 +90,12 @@ struct gsp_scale {
         gsp::ScaleTickArgs a{};
         a.prev = sh.table[(t + 1) & 1].p;
         a.cur = sh.table[t & 1].p;
-        a.remote = nullptr;
+        a.remote = rowmode ? reinterpret_cast<const uint16_t *>(sh.x.recv_rows.p) : nullptr;
         a.stride = stride;
         a.n = p.n;
         a.col0 = sh.col0;
-        a.row0 = 0;
-        a.rows = p.n;
+        a.row0 = sh.row0;
+        a.rows = sh.rows;
         a.tick = t;
         a.tremove = p.tremove;
         a.fanout = p.fanout;
@@ -95,7 +103,7 @@ struct gsp_scale {
         a.h0 = p.h0;
         a.nt_own = policy & 1;
         a.nt_src = (policy >> 1) & 1;
-        a.count_rounds = sh.g == 0;
+        a.count_rounds = rowmode || sh.g == 0;
         a.seed = p.seed;
         a.fail_tick = sh.fail_tick.p;
         a.own_hb = sh.own_hb.p;
@@ -103,7 +111,7 @@ struct gsp_scale {
         a.cnt_cur = sliced ? sh.cnt_slice.p : sh.cnt_total[t & 1].p;
         a.off = sh.off.p;
         a.csr_src = sh.csr_src.p;
-        a.csr_slot = nullptr;
+        a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
         a.out_dst = sh.out_dst.p;
         a.deg = sh.deg.p;
         a.bitmap = sh.bitmap.p;
@@ -176,19 +184,20 @@ namespace {
 
 int shard_alloc(gsp_scale *s, Shard &sh) {
     const int32_t n = s->p.n;
-    const size_t tab = size_t(n) * size_t(s->stride);
+    const size_t rows = size_t(sh.rows);
+    const size_t tab = rows * size_t(s->stride);
     hipStream_t st = s->st;
     for (int b = 0; b < 2; ++b) {
         GSP_HIP(sh.table[b].alloc(tab));
         GSP_HIP(sh.cnt_total[b].alloc(size_t(n)));
         GSP_HIP(hipMemsetAsync(sh.cnt_total[b].p, 0, size_t(n) * 4, st));
     }
-    GSP_HIP(sh.own_hb.alloc(size_t(n)));
+    GSP_HIP(sh.own_hb.alloc(rows));
     GSP_HIP(sh.fail_tick.alloc(size_t(n)));
-    GSP_HIP(sh.out_dst.alloc(size_t(n) * s->p.fanout));
+    GSP_HIP(sh.out_dst.alloc(rows * s->p.fanout));
     GSP_HIP(sh.deg.alloc(size_t(n)));
-    GSP_HIP(sh.off.alloc(size_t(n) + 1));
-    GSP_HIP(sh.fill.alloc(size_t(n)));
+    GSP_HIP(sh.off.alloc(rows + 1));
+    GSP_HIP(sh.fill.alloc(rows));
     GSP_HIP(sh.csr_src.alloc(size_t(n) * s->p.fanout));
     GSP_HIP(sh.err.alloc(1));
     GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
@@ -198,10 +207,13 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
         GSP_HIP(sh.picks.alloc(size_t(n) * s->p.fanout));
         GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8)));
     }
+    if (s->rowmode)
+        GSP_HIP(sh.x.alloc(s->shards, s->pair_cap, s->msg_cap, int32_t(s->stride / 4),
+                           int64_t(n) * s->p.fanout, st));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(sh.dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
-    GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, size_t(n) * 4, st));
+    GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
     GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, st));
     GSP_HIP(hipMemsetAsync(sh.err.p, 0, 4, st));
     GSP_HIP(hipMemcpyAsync(sh.fail_tick.p, s->h_fail.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
@@ -254,6 +266,45 @@ int resolve_sends(gsp_scale *s, int32_t t) {
     return GSP_OK;
 }
 
+// Row layout: every shard's member counts of tick t (cnt_total[t & 1], own rows only) reach
+// every shard -- the merges digest of tick t + 1 reads them for remote senders.
+int exchange_row_counts(gsp_scale *s, int32_t t) {
+    if (s->comm) {
+        Shard &sh = s->local[0];
+        int32_t *cnt = sh.cnt_total[t & 1].p;
+        GSP_NCCL(ncclGroupStart());
+        for (int32_t g = 0; g < s->shards; ++g) {
+            const int32_t r0 = gsp::rowx_row0(g, s->p.n, s->shards);
+            const int32_t nr = gsp::rowx_row0(g + 1, s->p.n, s->shards) - r0;
+            GSP_NCCL(ncclBroadcast(cnt + r0, cnt + r0, size_t(nr), ncclInt32, g, s->comm, s->st));
+        }
+        GSP_NCCL(ncclGroupEnd());
+        s->perf.xgmi_bytes += double(sh.rows) * 4.0 * double(s->shards - 1);
+        return GSP_OK;
+    }
+    for (Shard &src : s->local)
+        for (Shard &dst : s->local) {
+            if (&src == &dst) continue;
+            GSP_HIP(hipMemcpyAsync(dst.cnt_total[t & 1].p + src.row0, src.cnt_total[t & 1].p + src.row0,
+                                   size_t(src.rows) * 4, hipMemcpyDeviceToDevice, s->st));
+            s->perf.xgmi_bytes += double(src.rows) * 4.0;
+        }
+    return GSP_OK;
+}
+
+// Row layout: the sender rows of tick t_sent's cross-shard messages move to their receivers'
+// shards (rowx_host.cpp); every shard gets the receiver CSR of tick t_sent + 1.
+int exchange_rows(gsp_scale *s, int32_t t_sent) {
+    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, int32_t(s->stride / 4), s->pair_cap,
+                     s->msg_cap, s->comm, s->st, s->h_cnt, s->h_recv};
+    std::vector<gsp::RowxShard> v;
+    for (Shard &sh : s->local)
+        v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p,
+                                   reinterpret_cast<const uint64_t *>(sh.table[t_sent & 1].p),
+                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p, &sh.x});
+    return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
+}
+
 int check_err(gsp_scale *s) {
     for (Shard &sh : s->local) {
         int32_t err = 0;
@@ -283,7 +334,7 @@ int collect_timing(gsp_scale *s) {
 }
 
 int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t rank,
-                int32_t local_shards, const void *nccl_id, gsp_scale **out) {
+                int32_t local_shards, const void *nccl_id, int32_t layout, gsp_scale **out) {
     GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_scale: out is NULL");
     *out = nullptr;
     if (int rc = gsp::validate_scale_params(p)) return rc;
@@ -298,11 +349,27 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     s->device = device;
     s->shards = shards;
     s->rank = rank;
-    // a communicator always runs the column protocol (with one rank it exercises RCCL alone)
-    s->sliced = shards > 1 || nccl_id != nullptr;
-    const int64_t unit = int64_t(gsp::kChunk) * shards;
+    GSP_REQUIRE(layout == GSP_SHARD_COLUMNS || layout == GSP_SHARD_ROWS, GSP_ERR_INVALID,
+                "gsp_scale: layout %d", layout);
+    GSP_REQUIRE(shards <= p->n, GSP_ERR_INVALID, "gsp_scale: %d shards for %d nodes", shards, p->n);
+    // a communicator always runs the sharded protocol (with one rank it exercises RCCL alone)
+    const bool sharded = shards > 1 || nccl_id != nullptr;
+    s->sliced = sharded && layout == GSP_SHARD_COLUMNS;
+    s->rowmode = sharded && layout == GSP_SHARD_ROWS;
+    const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
-    s->stride = s->width / shards;
+    s->stride = s->width / (s->sliced ? shards : 1);
+    if (s->rowmode) {
+        // a sender row goes to a shard at most once: rows_max pairs always fit; large rows get
+        // the expected share 1 - (1 - 1/G)^f with margin (a tick beyond it fails loudly)
+        int32_t rows_max = 0;
+        for (int32_t g = 0; g < shards; ++g)
+            rows_max = std::max(rows_max, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
+        const double share = 1.0 - std::pow(1.0 - 1.0 / shards, double(p->fanout));
+        s->pair_cap = std::min<int64_t>(rows_max, int64_t(rows_max * share * 1.1) + 1024);
+        s->msg_cap = std::min<int64_t>(int64_t(rows_max) * p->fanout,
+                                       int64_t(double(rows_max) * p->fanout / shards * 1.25) + 4096);
+    }
     s->h_fail = gsp::scale_fail_ticks(*p);
     if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 3;
     if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
@@ -313,6 +380,10 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                     (long long)(s->stride / 8));
     }
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    if (s->rowmode) {
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
+    }
     if (nccl_id) {
         ncclUniqueId id;
         std::memcpy(&id, nccl_id, sizeof id);
@@ -322,12 +393,16 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     for (int32_t i = 0; i < local_shards; ++i) {
         Shard &sh = s->local[size_t(i)];
         sh.g = rank + i;
-        sh.col0 = int32_t(int64_t(sh.g) * s->stride);
+        sh.col0 = s->sliced ? int32_t(int64_t(sh.g) * s->stride) : 0;
+        sh.row0 = s->rowmode ? gsp::rowx_row0(sh.g, p->n, shards) : 0;
+        sh.rows = s->rowmode ? gsp::rowx_row0(sh.g + 1, p->n, shards) - sh.row0 : p->n;
         if (int rc = shard_alloc(s.get(), sh)) return rc;
     }
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_init(s->args(sh, 0), s->sliced, s->st));
     if (s->sliced)
         if (int rc = resolve_sends(s.get(), 0)) return rc;
+    if (s->rowmode)
+        if (int rc = exchange_row_counts(s.get(), 0)) return rc;
     GSP_HIP(hipStreamSynchronize(s->st));
     *out = s.release();
     return GSP_OK;
@@ -338,11 +413,22 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
 extern "C" {
 
 int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out) {
-    return scale_build(p, device, 1, 0, 1, nullptr, out);
+    return scale_build(p, device, 1, 0, 1, nullptr, GSP_SHARD_COLUMNS, out);
 }
 
 int gsp_scale_create_group(const gsp_scale_params *p, int device, int32_t shards, gsp_scale **out) {
-    return scale_build(p, device, shards, 0, shards, nullptr, out);
+    return scale_build(p, device, shards, 0, shards, nullptr, GSP_SHARD_COLUMNS, out);
+}
+
+int gsp_scale_create_group_layout(const gsp_scale_params *p, int device, int32_t shards,
+                                  int32_t layout, gsp_scale **out) {
+    return scale_build(p, device, shards, 0, shards, nullptr, layout, out);
+}
+
+int gsp_scale_create_rank_layout(const gsp_scale_params *p, int device, int32_t rank,
+                                 int32_t world, const void *nccl_id, int32_t layout, gsp_scale **out) {
+    GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_scale_create_rank_layout: NULL nccl id");
+    return scale_build(p, device, world, rank, 1, nccl_id, layout, out);
 }
 
 int gsp_scale_nccl_id(void *out, size_t cap) {
@@ -357,7 +443,7 @@ int gsp_scale_nccl_id(void *out, size_t cap) {
 int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
                           const void *nccl_id, gsp_scale **out) {
     GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_scale_create_rank: NULL nccl id");
-    return scale_build(p, device, world, rank, 1, nccl_id, out);
+    return scale_build(p, device, world, rank, 1, nccl_id, GSP_SHARD_COLUMNS, out);
 }
 
 int gsp_scale_destroy(gsp_scale *s) {
@@ -372,6 +458,8 @@ int gsp_scale_destroy(gsp_scale *s) {
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
     for (Shard &sh : s->local) sh.release();
     if (s->comm) (void)ncclCommDestroy(s->comm);
+    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
+    if (s->h_recv) (void)hipHostFree(s->h_recv);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -391,12 +479,16 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
             tm = {s->event(), s->event(), s->event()};
             GSP_HIP(hipEventRecord(tm.a, s->st));
         }
-        for (Shard &sh : s->local) {
-            GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
-            GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
-            GSP_HIP(gsp::launch_scatter(sh.out_dst.p, slots, s->p.fanout, 0, sh.off.p, sh.fill.p,
-                                        sh.csr_src.p, s->st));
-            GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
+        if (s->rowmode) {
+            if (int rc = exchange_rows(s, t - 1)) return rc;
+        } else {
+            for (Shard &sh : s->local) {
+                GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
+                GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
+                GSP_HIP(gsp::launch_scatter(sh.out_dst.p, slots, s->p.fanout, 0, sh.off.p, sh.fill.p,
+                                            sh.csr_src.p, s->st));
+                GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
+            }
         }
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (Shard &sh : s->local)
@@ -407,6 +499,8 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
         }
         if (s->sliced)
             if (int rc = resolve_sends(s, t)) return rc;
+        if (s->rowmode)
+            if (int rc = exchange_row_counts(s, t)) return rc;
         s->tick = t;
         s->perf.ticks++;
     }
@@ -463,6 +557,15 @@ int gsp_scale_row(gsp_scale *s, int32_t r, uint16_t *buf, int32_t cap) {
     std::memset(buf, 0, size_t(s->p.n) * 2);
     // a crashed row stops at its fail tick: read the buffer of the last tick it ran
     const int32_t last = std::min(s->tick, s->h_fail[size_t(r)]);
+    if (s->rowmode) {
+        for (Shard &sh : s->local)
+            if (r >= sh.row0 && r < sh.row0 + sh.rows) {
+                GSP_HIP(hipMemcpy(buf, sh.table[last & 1].p + size_t(r - sh.row0) * size_t(s->stride),
+                                  size_t(s->p.n) * 2, hipMemcpyDeviceToHost));
+                return GSP_OK;
+            }
+        GSP_REQUIRE(false, GSP_ERR_INVALID, "gsp_scale_row: row %d is not held by this rank", r);
+    }
     for (Shard &sh : s->local) {
         const int64_t c0 = sh.col0;
         const int64_t cnt = std::min<int64_t>(s->stride, int64_t(s->p.n) - c0);
@@ -476,18 +579,35 @@ int gsp_scale_row(gsp_scale *s, int32_t r, uint16_t *buf, int32_t cap) {
 int gsp_scale_own_hb(gsp_scale *s, int32_t r, int32_t *hb) {
     GSP_REQUIRE(s && hb && r >= 0 && r < s->p.n, GSP_ERR_INVALID, "gsp_scale_own_hb: bad row");
     if (int rc = gsp_scale_sync(s)) return rc;
-    GSP_HIP(hipMemcpy(hb, s->local[0].own_hb.p + r, 4, hipMemcpyDeviceToHost));
+    for (Shard &sh : s->local)
+        if (r >= sh.row0 && r < sh.row0 + sh.rows) {
+            GSP_HIP(hipMemcpy(hb, sh.own_hb.p + (r - sh.row0), 4, hipMemcpyDeviceToHost));
+            return GSP_OK;
+        }
+    GSP_REQUIRE(false, GSP_ERR_INVALID, "gsp_scale_own_hb: row %d is not held by this rank", r);
     return GSP_OK;
 }
 
 int gsp_scale_messages(gsp_scale *s, int32_t *dst, int64_t cap, int64_t *n) {
     GSP_REQUIRE(s && n, GSP_ERR_INVALID, "gsp_scale_messages: NULL");
     if (int rc = gsp_scale_sync(s)) return rc;
-    const int64_t slots = int64_t(s->p.n) * s->p.fanout;
-    *n = slots;
-    if (dst && cap > 0)
-        GSP_HIP(hipMemcpy(dst, s->local[0].out_dst.p, size_t(std::min(cap, slots)) * 4,
-                          hipMemcpyDeviceToHost));
+    if (!s->rowmode) {
+        const int64_t slots = int64_t(s->p.n) * s->p.fanout;
+        *n = slots;
+        if (dst && cap > 0)
+            GSP_HIP(hipMemcpy(dst, s->local[0].out_dst.p, size_t(std::min(cap, slots)) * 4,
+                              hipMemcpyDeviceToHost));
+        return GSP_OK;
+    }
+    int64_t total = 0;          // row layout: the slots of the rows held here, in row order
+    for (Shard &sh : s->local) {
+        const int64_t slots = int64_t(sh.rows) * s->p.fanout;
+        if (dst && total < cap)
+            GSP_HIP(hipMemcpy(dst + total, sh.out_dst.p, size_t(std::min(cap - total, slots)) * 4,
+                              hipMemcpyDeviceToHost));
+        total += slots;
+    }
+    *n = total;
     return GSP_OK;
 }
 
@@ -502,7 +622,7 @@ int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out) {
     // one sender row per delivered message (stride * 2 B) and its CSR entry (4 B)
     const double rows = double(2 * d.node_rounds + d.delivered);
     s->perf.bytes_per_tick = (rows * double(s->stride) * 2.0 + double(d.delivered) * 4.0) *
-                             double(s->local.size());
+                             double(s->sliced ? s->local.size() : 1);
     *out = s->perf;
     return GSP_OK;
 }

@@ -10,6 +10,7 @@ from . import _lib
 from ._lib import check, lib
 
 FAIL_NONE, FAIL_RANDOM, FAIL_BLOCK = 0, 1, 2
+LAYOUTS = {"columns": 0, "rows": 1}
 
 
 def unpack(entries):
@@ -28,26 +29,29 @@ def nccl_unique_id():
 class ScaleEngine:
     """One scale engine.
 
-    group=G (> 1): G column shards inside this process on `device` (exchange by device
-    copies).  rank/world/nccl_id: this process holds column shard `rank` of `world`
-    (exchange over RCCL).  Default: one GPU, full rows, fused tick kernel.
+    group=G (> 1): G shards inside this process on `device` (exchange by device copies).
+    rank/world/nccl_id: this process holds shard `rank` of `world` (exchange over RCCL).
+    layout: "columns" (column slices of every row) or "rows" (row blocks; sender rows move
+    between shards).  Default: one GPU, full rows, fused tick kernel.
     """
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
                  fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0, group=1,
-                 rank=0, world=1, nccl_id=None):
+                 rank=0, world=1, nccl_id=None, layout="columns"):
         self.params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
                                           h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
                                           fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks)
         self._h = ctypes.c_void_p()
+        lay = LAYOUTS[layout]
         if nccl_id is not None:
             idbuf = ctypes.create_string_buffer(nccl_id, 128)
-            check(lib().gsp_scale_create_rank(ctypes.byref(self.params), device, rank, world,
-                                              idbuf, ctypes.byref(self._h)),
-                  "gsp_scale_create_rank")
+            check(lib().gsp_scale_create_rank_layout(ctypes.byref(self.params), device, rank, world,
+                                                     idbuf, lay, ctypes.byref(self._h)),
+                  "gsp_scale_create_rank_layout")
         elif group > 1:
-            check(lib().gsp_scale_create_group(ctypes.byref(self.params), device, group,
-                                               ctypes.byref(self._h)), "gsp_scale_create_group")
+            check(lib().gsp_scale_create_group_layout(ctypes.byref(self.params), device, group, lay,
+                                                      ctypes.byref(self._h)),
+                  "gsp_scale_create_group_layout")
         else:
             check(lib().gsp_scale_create(ctypes.byref(self.params), device, ctypes.byref(self._h)),
                   "gsp_scale_create")

@@ -229,7 +229,22 @@ int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, i
                           const void *nccl_id, gsp_scale **out);
 int gsp_scale_create_group(const gsp_scale_params *p, int device, int32_t shards,
                            gsp_scale **out);
-/* shards of the job, first shard index held by this engine, columns per shard */
+/* Sharding layout of a multi-shard job.
+ *   GSP_SHARD_COLUMNS  shard g owns a column slice of every row (above; O(n) exchange)
+ *   GSP_SHARD_ROWS     shard g owns rows [floor(g n / G), floor((g + 1) n / G)); each tick the
+ *                      sender rows that messages carry to another shard move there once per
+ *                      (sender, shard) by RCCL send/recv, with the message records, and the
+ *                      member counts of every row are broadcast (DESIGN.md "Multi-GPU").
+ * Results are identical to gsp_scale_create in both layouts.  In the row layout
+ * gsp_scale_row / gsp_scale_own_hb fail with GSP_ERR_INVALID for a row another rank holds and
+ * gsp_scale_messages returns the slots of the rows held here, in row order. */
+typedef enum { GSP_SHARD_COLUMNS = 0, GSP_SHARD_ROWS = 1 } gsp_shard_layout;
+int gsp_scale_create_rank_layout(const gsp_scale_params *p, int device, int32_t rank,
+                                 int32_t world, const void *nccl_id, int32_t layout, gsp_scale **out);
+int gsp_scale_create_group_layout(const gsp_scale_params *p, int device, int32_t shards,
+                                  int32_t layout, gsp_scale **out);
+/* shards of the job, first shard index held by this engine, columns per shard (row layout:
+ * the full row stride) */
 int gsp_scale_layout(gsp_scale *s, int32_t *shards, int32_t *rank, int64_t *stride);
 int gsp_scale_destroy(gsp_scale *s);
 /* Advance `ticks` ticks on the device (no host synchronisation inside). */

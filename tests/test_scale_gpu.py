@@ -36,29 +36,34 @@ def _compare_state(eng, orc, n, rows):
 
 
 VARIANTS = {
-    # name: (column shards in one process, packed merge, cache policy)
-    "fused": (1, 1, 1),
-    "fused_scalar_merge": (1, 0, 0),
-    "fused_nt_all": (1, 1, 3),
-    "columns2": (2, 1, 1),
-    "columns3": (3, 1, 1),
-    "columns4_scalar": (4, 0, 2),
+    # name: (shards in one process, layout, packed merge, cache policy)
+    "fused": (1, "columns", 1, 1),
+    "fused_scalar_merge": (1, "columns", 0, 0),
+    "fused_nt_all": (1, "columns", 1, 3),
+    "columns2": (2, "columns", 1, 1),
+    "columns3": (3, "columns", 1, 1),
+    "columns4_scalar": (4, "columns", 0, 2),
+    "rows2": (2, "rows", 1, 1),
+    "rows3": (3, "rows", 1, 1),
+    "rows8_scalar": (8, "rows", 0, 2),
 }
 VARIANT_CASES = [(c, "fused") for c in CASES] + [
     (CASES[1], "fused_scalar_merge"), (CASES[3], "fused_nt_all"), (CASES[1], "columns2"),
-    (CASES[3], "columns3"), (CASES[4], "columns2"), (CASES[2], "columns4_scalar")]
+    (CASES[3], "columns3"), (CASES[4], "columns2"), (CASES[2], "columns4_scalar"),
+    (CASES[0], "rows2"), (CASES[1], "rows3"), (CASES[3], "rows2"), (CASES[4], "rows3"),
+    (CASES[2], "rows8_scalar")]
 
 
 @pytest.mark.parametrize("case,variant", VARIANT_CASES,
                          ids=lambda x: x if isinstance(x, str) else "n%d_f%d_d%d_m%d" % x[:4])
 def test_scale_matches_oracle(case, variant):
     n, f, drop, mode, ftick, ppm, seed, ticks = case
-    group, packed, policy = VARIANTS[variant]
+    group, layout, packed, policy = VARIANTS[variant]
     orc = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
                       seed=seed)
     rng = np.random.default_rng(seed)
     with ScaleEngine(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
-                     seed=seed, max_ticks=ticks, group=group) as eng:
+                     seed=seed, max_ticks=ticks, group=group, layout=layout) as eng:
         eng.set_merge(packed)
         eng.set_cache_policy(policy)
         # tick-0 sends (pre-joined bootstrap)
@@ -81,6 +86,8 @@ def test_scale_matches_oracle(case, variant):
         _compare_state(eng, orc, n, range(n) if n <= 512 else range(0, n, 61))
         perf = eng.perf()
         assert perf["ticks"] == ticks and perf["merge_ms"] > 0
+        if layout == "rows" and group > 1:
+            assert perf["xgmi_bytes"] > 0
 
 
 def test_rccl_rank_path_one_rank():
@@ -117,6 +124,44 @@ def test_columns_equal_fused_full_size():
             assert np.array_equal(b.row(r), row), r
         assert np.array_equal(b.messages(), ma)
     assert da == db
+
+
+def test_rows_equal_fused_full_size():
+    """Config-3 size: 4 row shards (in-process: the pack / gather / CSR kernels of the RCCL
+    row path, exchange by device copies) give the one-GPU results."""
+    n, ticks = 65536, 14
+    kw = dict(fanout=3, fail_mode=FAIL_RANDOM, fail_tick=10, fail_ppm=10000, seed=0x5EED,
+              max_ticks=ticks)
+    with ScaleEngine(n, **kw) as a:
+        a.step(ticks)
+        da = [a.digest(t) for t in range(1, ticks + 1)]
+        ra = {r: a.row(r) for r in (0, 16383, 16384, 40000, n - 1)}
+        ma = a.messages()
+    with ScaleEngine(n, group=4, layout="rows", **kw) as b:
+        b.step(ticks)
+        db = [b.digest(t) for t in range(1, ticks + 1)]
+        for r, row in ra.items():
+            assert np.array_equal(b.row(r), row), r
+        assert np.array_equal(b.messages(), ma)
+        assert b.perf()["xgmi_bytes"] > 0
+    assert da == db
+
+
+def test_rccl_rows_one_rank():
+    """The RCCL row path (count broadcasts, all-gather, send/recv group with no peers) with a
+    world of one matches the oracle."""
+    from gossip_protocol_amd.scale import nccl_unique_id
+    n, ticks = 1500, 14
+    orc = ScaleOracle(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5,
+                      fail_ppm=20000, seed=8)
+    with ScaleEngine(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5, fail_ppm=20000,
+                     seed=8, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id(),
+                     layout="rows") as eng:
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, t
+        _compare_state(eng, orc, n, range(0, n, 37))
 
 
 def test_scale_full_size_properties():
