@@ -160,13 +160,13 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     return out
 
 
-def run_full(nodes, steps, warmup, world, local, dist):
-    """Full-view workload (config 3 rules) on `world` GPUs: one GPU fused, or column shards.
-    Returns job totals (time and kernel time are the slowest rank's)."""
+def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
+    """Full-view workload (config 3 rules) on `world` GPUs: one GPU fused, or column / row
+    shards.  Returns job totals (time and kernel time are the slowest rank's)."""
     import torch
     from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
     kw = dict(fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM,
-              seed=SEED, max_ticks=warmup + steps)
+              seed=SEED, max_ticks=warmup + steps, layout=layout)
     if dist is not None:
         from gossip_protocol_amd.dist import make_rank_engine
         eng = make_rank_engine(nodes, local, **kw)
@@ -199,8 +199,9 @@ def run_full(nodes, steps, warmup, world, local, dist):
     csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / launches
     eng.close()
     if dist is not None:
-        # per-row counts live on rank 0 only (sum = job total); the step and kernel times are
-        # the slowest rank's (max); every rank sends its own exchange bytes (sum)
+        # per-row counts live on rank 0 only (columns) or on the row's owner (rows): the sum is
+        # the job total; the step and kernel times are the slowest rank's (max); every rank
+        # sends its own exchange bytes (sum)
         u = torch.tensor([rounds, merges, delivered, xgmi_tick], dtype=torch.float64,
                          device=_dev())
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
@@ -209,11 +210,13 @@ def run_full(nodes, steps, warmup, world, local, dist):
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         el, kern_ms, csr_ms = (x.item() for x in m)
     # algorithmic bytes per launch: own row read + write and one sender row per message
-    # (2-byte entries), one 4-byte CSR entry per message; every shard streams its slice
-    # (stride columns) of each such row, so the job moves `world` slices
-    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * world / steps
+    # (2-byte entries), one 4-byte CSR entry per message; column shards stream their slice
+    # (stride columns) of each such row, so the job moves `world` slices; row shards stream
+    # whole rows (stride = full width) of their own receivers only
+    slices = world if layout == "columns" else 1
+    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
     return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
-            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick}
+            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout}
 
 
 def summarize_full(r, nodes, steps, world):
@@ -235,12 +238,13 @@ def summarize_full(r, nodes, steps, world):
         "config": {"workload": "%s: %d nodes full view, fanout %d, 1%% random crash at t=%d, "
                                "no drops" % (cfg, nodes, FANOUT, FAIL_TICK),
                    "nodes": nodes, "view": nodes, "fanout": FANOUT, "entry_bytes": 2,
-                   "parallelism": "columns%d" % world if world > 1 else "1gpu"},
+                   "parallelism": "%s%d" % (r["layout"], world) if world > 1 else "1gpu"},
         "merges_per_s": r["merges"] / r["el"],
         "xgmi_bytes_per_tick": r["xgmi_tick"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
-                     "kernel_ms": r["kern_ms"], "csr_ms": r["csr_ms"],
+                     "kernel_ms": r["kern_ms"],
+                     ("exchange_csr_ms" if r["layout"] == "rows" else "csr_ms"): r["csr_ms"],
                      "algorithmic_bytes_per_launch": r["bytes_per_launch"]},
     }
 
@@ -267,6 +271,8 @@ def main(argv=None):
     ap.add_argument("--no-pview", action="store_true", help="skip the config-5 line item")
     ap.add_argument("--pview-nodes", type=int, default=PV_NODES)
     ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item (N > 1)")
+    ap.add_argument("--no-rows", action="store_true",
+                    help="skip the full-view row-layout line items (N > 1)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -290,6 +296,21 @@ def main(argv=None):
         # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)
         r = run_full(262144, min(args.steps, 8), 2, world, local, dist)
         f262 = summarize_full(r, 262144, min(args.steps, 8), world)
+    rows = {}
+    if world > 1 and not args.no_rows:
+        # the full view ROW-sharded (north star: sender rows cross shards over RCCL send/recv,
+        # deduplicated per (sender, shard)); O(f n^2) xGMI bytes per tick against the column
+        # layout's O(n), reported beside it (DESIGN.md "Multi-GPU")
+        r = run_full(args.nodes, min(args.steps, 8), 2, world, local, dist, layout="rows")
+        rows["config3"] = summarize_full(r, args.nodes, min(args.steps, 8), world)
+        if not args.no_262k:
+            if world >= 4:
+                r = run_full(262144, 4, 2, world, local, dist, layout="rows")
+                rows["config4"] = summarize_full(r, 262144, 4, world)
+            else:
+                # 2 x 68.7 GB of table rows plus ~2 x 66 GB of send/receive rows per GPU
+                rows["config4"] = {"skipped": "row layout at 262,144 nodes needs > 270 GB per "
+                                              "GPU at N = 2 (tables + exchange regions)"}
 
     if rank == 0:
         out = summarize_full(full, args.nodes, args.steps, world)
@@ -301,6 +322,8 @@ def main(argv=None):
             out["pview"] = pv
         if f262 is not None:
             out["full262k"] = f262
+        if rows:
+            out["full_rows"] = rows
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -14,17 +14,17 @@ namespace gsp {
 
 hipError_t RowxBufs::alloc(int32_t shards, int64_t pair_cap, int64_t msg_cap, int32_t row_words,
                            int64_t csr_cap, hipStream_t st) {
-    const size_t G = size_t(shards);
+    const size_t G = size_t(shards), R = size_t(shards > 1 ? shards - 1 : 1);   // regions
     hipError_t e;
     if ((e = cnt.alloc(2 * G)) != hipSuccess) return e;
     if ((e = cnt_all.alloc(2 * G * G)) != hipSuccess) return e;
     if ((e = recv_msgs.alloc(G)) != hipSuccess) return e;
-    if ((e = pair_row.alloc(G * size_t(pair_cap))) != hipSuccess) return e;
+    if ((e = pair_row.alloc(R * size_t(pair_cap))) != hipSuccess) return e;
     if ((e = csr_slot.alloc(size_t(csr_cap))) != hipSuccess) return e;
-    if ((e = send_rows.alloc(G * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
-    if ((e = recv_rows.alloc(G * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
-    if ((e = send_rec.alloc(G * size_t(msg_cap))) != hipSuccess) return e;
-    if ((e = recv_rec.alloc(G * size_t(msg_cap))) != hipSuccess) return e;
+    if ((e = send_rows.alloc(R * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
+    if ((e = recv_rows.alloc(R * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
+    if ((e = send_rec.alloc(R * size_t(msg_cap))) != hipSuccess) return e;
+    if ((e = recv_rec.alloc(R * size_t(msg_cap))) != hipSuccess) return e;
     return hipMemsetAsync(recv_msgs.p, 0, G * 4, st);
 }
 
@@ -88,7 +88,8 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
         GSP_NCCL(ncclGroupStart());
         for (int32_t h = 0; h < G; ++h) {
             if (h == me) continue;
-            const size_t so = size_t(h) * size_t(job.pair_cap), mo = size_t(h) * size_t(job.msg_cap);
+            const size_t reg = size_t(rowx_region(h, me));      // same index for h's region here
+            const size_t so = reg * size_t(job.pair_cap), mo = reg * size_t(job.msg_cap);
             if (pairs(me, h))
                 GSP_NCCL(ncclSend(sh.x->send_rows.p + so * W, size_t(pairs(me, h)) * W, ncclUint64, h,
                                   job.comm, st));
@@ -109,8 +110,10 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
             for (RowxShard &dst : local) {
                 const int32_t g = src.g, h = dst.g;
                 if (g == h) continue;
-                const size_t so = size_t(h) * size_t(job.pair_cap), mo = size_t(h) * size_t(job.msg_cap);
-                const size_t ro = size_t(g) * size_t(job.pair_cap), qo = size_t(g) * size_t(job.msg_cap);
+                // src's region for h (send side), dst's region for g (receive side)
+                const size_t sr = size_t(rowx_region(h, g)), rr = size_t(rowx_region(g, h));
+                const size_t so = sr * size_t(job.pair_cap), mo = sr * size_t(job.msg_cap);
+                const size_t ro = rr * size_t(job.pair_cap), qo = rr * size_t(job.msg_cap);
                 if (pairs(g, h))
                     GSP_HIP(hipMemcpyAsync(dst.x->recv_rows.p + ro * W, src.x->send_rows.p + so * W,
                                            size_t(pairs(g, h)) * row_bytes, hipMemcpyDeviceToDevice, st));
@@ -126,15 +129,15 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
         int32_t *hr = job.h_recv + i * size_t(G);
         for (int32_t h = 0; h < G; ++h) hr[h] = h == sh.g ? 0 : int32_t(msgs(h, sh.g));
         GSP_HIP(hipMemcpyAsync(sh.x->recv_msgs.p, hr, size_t(G) * 4, hipMemcpyHostToDevice, st));
-        GSP_HIP(launch_rowx_recv_deg(sh.x->recv_rec.p, sh.x->recv_msgs.p, G, job.msg_cap, sh.row0,
-                                     sh.deg, st));
+        GSP_HIP(launch_rowx_recv_deg(sh.x->recv_rec.p, sh.x->recv_msgs.p, G, sh.g, job.msg_cap,
+                                     sh.row0, sh.deg, st));
         GSP_HIP(launch_exclusive_scan(sh.deg + sh.row0, sh.off, sh.rows, sh.tile_sum, st));
         GSP_HIP(hipMemsetAsync(sh.fill, 0, size_t(sh.rows) * 4, st));
         GSP_HIP(launch_rowx_scatter_local(sh.out_dst, sh.rows, F, sh.row0, sh.off, sh.fill, sh.csr_src,
                                           sh.x->csr_slot.p, st));
-        GSP_HIP(launch_rowx_scatter_remote(sh.x->recv_rec.p, sh.x->recv_msgs.p, G, job.msg_cap,
-                                           job.pair_cap, sh.off, sh.fill, sh.csr_src, sh.x->csr_slot.p,
-                                           st));
+        GSP_HIP(launch_rowx_scatter_remote(sh.x->recv_rec.p, sh.x->recv_msgs.p, G, sh.g,
+                                           job.msg_cap, job.pair_cap, sh.off, sh.fill, sh.csr_src,
+                                           sh.x->csr_slot.p, st));
         GSP_HIP(hipMemsetAsync(sh.deg, 0, size_t(job.n) * 4, st));
     }
     return GSP_OK;

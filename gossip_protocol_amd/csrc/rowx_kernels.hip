@@ -60,14 +60,15 @@ __global__ void __launch_bounds__(256) rowx_pack_kernel(RowxArgs a) {
         // counts keep growing past the capacity (the host sees them and fails the tick);
         // nothing is written out of bounds
         const int32_t p = pbase + int32_t(__popcll(pm & ((1ull << lane) - 1ull)));
-        if (p < a.pair_cap) a.pair_row[int64_t(h) * a.pair_cap + p] = lr;
+        const int64_t reg = rowx_region(h, a.shard);
+        if (p < a.pair_cap) a.pair_row[reg * a.pair_cap + p] = lr;
         int32_t m = mbase + int32_t(mpre);
         const int32_t hrow0 = rowx_row0(h, a.n, a.shards);
 #pragma unroll
         for (int k = 0; k < kMaxFanout; ++k)
             if (h_of[k] == h) {
                 if (m < a.msg_cap && p < a.pair_cap)
-                    a.send_rec[int64_t(h) * a.msg_cap + m] = RowxRec{a.row0 + lr, d_of[k] - hrow0, p};
+                    a.send_rec[reg * a.msg_cap + m] = RowxRec{a.row0 + lr, d_of[k] - hrow0, p};
                 m++;
             }
     }
@@ -80,24 +81,29 @@ __global__ void __launch_bounds__(256) rowx_gather_kernel(RowxArgs a) {
     const int64_t nw = (int64_t(gridDim.x) * 256) >> 6;
     const int32_t W = a.row_words;
     for (int32_t h = 0; h < a.shards; ++h) {
+        if (h == a.shard) continue;
+        const int64_t reg = rowx_region(h, a.shard);
         const int64_t cnt = a.pair_cnt[h] < a.pair_cap ? a.pair_cnt[h] : a.pair_cap;
         for (int64_t p = w0; p < cnt; p += nw) {
-            const int32_t lr = a.pair_row[int64_t(h) * a.pair_cap + p];
+            const int32_t lr = a.pair_row[reg * a.pair_cap + p];
             const uint64_t *src = a.table + int64_t(lr) * W;
-            uint64_t *dst = a.send_rows + (int64_t(h) * a.pair_cap + p) * W;
+            uint64_t *dst = a.send_rows + (reg * a.pair_cap + p) * W;
             for (int32_t i = lane; i < W; i += 64) dst[i] = __builtin_nontemporal_load(src + i);
         }
     }
 }
 
 __global__ void __launch_bounds__(256) rowx_recv_deg_kernel(const RowxRec *rec, const int32_t *cnt,
-                                                            int32_t shards, int64_t msg_cap,
-                                                            int32_t row0, int32_t *deg) {
+                                                            int32_t shards, int32_t self,
+                                                            int64_t msg_cap, int32_t row0,
+                                                            int32_t *deg) {
     const int64_t i0 = int64_t(blockIdx.x) * 256 + threadIdx.x;
     const int64_t step = int64_t(gridDim.x) * 256;
     for (int32_t h = 0; h < shards; ++h) {
+        if (h == self) continue;
         const int64_t m = cnt[h];
-        for (int64_t i = i0; i < m; i += step) atomicAdd(&deg[row0 + rec[int64_t(h) * msg_cap + i].dst], 1);
+        const RowxRec *rh = rec + rowx_region(h, self) * msg_cap;
+        for (int64_t i = i0; i < m; i += step) atomicAdd(&deg[row0 + rh[i].dst], 1);
     }
 }
 
@@ -118,19 +124,21 @@ __global__ void __launch_bounds__(256) rowx_scatter_local_kernel(const int32_t *
 }
 
 __global__ void __launch_bounds__(256) rowx_scatter_remote_kernel(const RowxRec *rec, const int32_t *cnt,
-                                                                  int32_t shards, int64_t msg_cap,
-                                                                  int64_t pair_cap, const int32_t *off,
-                                                                  int32_t *fill, int32_t *csr_src,
-                                                                  int32_t *csr_slot) {
+                                                                  int32_t shards, int32_t self,
+                                                                  int64_t msg_cap, int64_t pair_cap,
+                                                                  const int32_t *off, int32_t *fill,
+                                                                  int32_t *csr_src, int32_t *csr_slot) {
     const int64_t i0 = int64_t(blockIdx.x) * 256 + threadIdx.x;
     const int64_t step = int64_t(gridDim.x) * 256;
     for (int32_t h = 0; h < shards; ++h) {
+        if (h == self) continue;
         const int64_t m = cnt[h];
+        const int64_t reg = rowx_region(h, self);
         for (int64_t i = i0; i < m; i += step) {
-            const RowxRec r = rec[int64_t(h) * msg_cap + i];
+            const RowxRec r = rec[reg * msg_cap + i];
             const int32_t pos = off[r.dst] + atomicAdd(&fill[r.dst], 1);
             csr_src[pos] = r.src;
-            csr_slot[pos] = -int32_t(int64_t(h) * pair_cap + r.pair) - 1;
+            csr_slot[pos] = -int32_t(reg * pair_cap + r.pair) - 1;
         }
     }
 }
@@ -157,9 +165,10 @@ hipError_t launch_rowx_gather(const RowxArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_rowx_recv_deg(const RowxRec *recv_rec, const int32_t *recv_msgs, int32_t shards,
-                                int64_t msg_cap, int32_t row0, int32_t *deg, hipStream_t st) {
+                                int32_t self, int64_t msg_cap, int32_t row0, int32_t *deg,
+                                hipStream_t st) {
     hipLaunchKernelGGL(rowx_recv_deg_kernel, dim3(blocks_for(msg_cap, 4096)), dim3(256), 0, st,
-                       recv_rec, recv_msgs, shards, msg_cap, row0, deg);
+                       recv_rec, recv_msgs, shards, self, msg_cap, row0, deg);
     return hipGetLastError();
 }
 
@@ -172,11 +181,12 @@ hipError_t launch_rowx_scatter_local(const int32_t *out_dst, int32_t rows, int32
 }
 
 hipError_t launch_rowx_scatter_remote(const RowxRec *recv_rec, const int32_t *recv_msgs,
-                                      int32_t shards, int64_t msg_cap, int64_t pair_cap,
-                                      const int32_t *off, int32_t *fill, int32_t *csr_src,
-                                      int32_t *csr_slot, hipStream_t st) {
+                                      int32_t shards, int32_t self, int64_t msg_cap,
+                                      int64_t pair_cap, const int32_t *off, int32_t *fill,
+                                      int32_t *csr_src, int32_t *csr_slot, hipStream_t st) {
     hipLaunchKernelGGL(rowx_scatter_remote_kernel, dim3(blocks_for(msg_cap, 4096)), dim3(256), 0, st,
-                       recv_rec, recv_msgs, shards, msg_cap, pair_cap, off, fill, csr_src, csr_slot);
+                       recv_rec, recv_msgs, shards, self, msg_cap, pair_cap, off, fill, csr_src,
+                       csr_slot);
     return hipGetLastError();
 }
 

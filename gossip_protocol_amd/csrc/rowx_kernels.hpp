@@ -10,9 +10,10 @@
 //   (host)   counts all-gathered, then RCCL send/recv of rows and records (or device copies
 //            between the shards of an in-process group);
 //   csr      receiver CSR over the local rows: local messages (csr_slot = local row) and
-//            received records (csr_slot = -(h * pair_cap + pair) - 1 into the remote rows).
-// HBM layout per shard: send_rows[G][pair_cap][row_words], send_rec[G][msg_cap],
-// recv_rows[G][pair_cap][row_words], recv_rec[G][msg_cap].  pair_cap = max rows of a shard
+//            received records (csr_slot = -(region * pair_cap + pair) - 1 into the remote rows).
+// HBM layout per shard, one REGION per other shard (rowx_region; none for the shard itself):
+// send_rows[G-1][pair_cap][row_words], send_rec[G-1][msg_cap], recv_rows[G-1][pair_cap]
+// [row_words], recv_rec[G-1][msg_cap].  pair_cap = max rows of a shard
 // makes every tick fit (a sender row goes to a shard at most once); an engine may size it
 // smaller for large rows, in which case a count above the capacity fails the tick
 // (GSP_ERR_CAPACITY) and nothing is written out of bounds.
@@ -37,9 +38,9 @@ struct RowxArgs {
     const uint64_t *table;           // this shard's rows of the tick the messages were sent in
     int32_t *pair_cnt;               // [G] pairs per destination shard (zeroed before pack)
     int32_t *msg_cnt;                // [G] records per destination shard
-    int32_t *pair_row;               // [G][pair_cap] local row of each pair
-    uint64_t *send_rows;             // [G][pair_cap][row_words]
-    RowxRec *send_rec;               // [G][msg_cap]
+    int32_t *pair_row;               // [G-1][pair_cap] local row of each pair
+    uint64_t *send_rows;             // [G-1][pair_cap][row_words]
+    RowxRec *send_rec;               // [G-1][msg_cap]
 };
 
 // owner shard of a global node id
@@ -50,19 +51,26 @@ __host__ __device__ inline int32_t rowx_row0(int32_t g, int32_t n, int32_t shard
     return int32_t(int64_t(g) * n / shards);
 }
 
+// region of peer shard h != self in a shard's send / receive buffers
+__host__ __device__ inline int64_t rowx_region(int32_t h, int32_t self) {
+    return h < self ? h : h - 1;
+}
+
 hipError_t launch_rowx_pack(const RowxArgs &a, hipStream_t st);
 hipError_t launch_rowx_gather(const RowxArgs &a, hipStream_t st);
-// deg[row0 + rec.dst]++ for the received records of every source shard (counts: recv_msgs[h])
+// deg[row0 + rec.dst]++ for the received records of every source shard h != self
+// (counts: recv_msgs[h])
 hipError_t launch_rowx_recv_deg(const RowxRec *recv_rec, const int32_t *recv_msgs, int32_t shards,
-                                int64_t msg_cap, int32_t row0, int32_t *deg, hipStream_t st);
+                                int32_t self, int64_t msg_cap, int32_t row0, int32_t *deg,
+                                hipStream_t st);
 // local messages: csr_src = sender id, csr_slot = sender's local row
 hipError_t launch_rowx_scatter_local(const int32_t *out_dst, int32_t rows, int32_t fanout,
                                      int32_t row0, const int32_t *off, int32_t *fill,
                                      int32_t *csr_src, int32_t *csr_slot, hipStream_t st);
-// received records: csr_slot = -(h * pair_cap + pair) - 1
+// received records: csr_slot = -(rowx_region(h, self) * pair_cap + pair) - 1
 hipError_t launch_rowx_scatter_remote(const RowxRec *recv_rec, const int32_t *recv_msgs,
-                                      int32_t shards, int64_t msg_cap, int64_t pair_cap,
-                                      const int32_t *off, int32_t *fill, int32_t *csr_src,
-                                      int32_t *csr_slot, hipStream_t st);
+                                      int32_t shards, int32_t self, int64_t msg_cap,
+                                      int64_t pair_cap, const int32_t *off, int32_t *fill,
+                                      int32_t *csr_src, int32_t *csr_slot, hipStream_t st);
 
 }  // namespace gsp

@@ -3,7 +3,8 @@
 The engines are replaced by deterministic fakes (the real ones need a GPU), so what runs is
 bench.py's own multi-rank logic: barriers around the timed region, the max-over-ranks time
 and kernel time, the job-total node-rounds / bytes / xGMI reductions, the three line items
-(config 3 headline, config 5 `pview`, config 4 `full262k`) and the single rank-0 JSON line.
+(config 3 headline, config 5 `pview`, config 4 `full262k`, the row-layout `full_rows`) and the
+single rank-0 JSON line.
 """
 import io
 import json
@@ -21,8 +22,8 @@ class FakeEngine:
     """Per-tick digest: `rows` node-rounds on rank 0 (column shards count rows on shard 0),
     2 deliveries per round; kernel 2 ms (rank 0) / 3 ms (rank 1) per tick."""
 
-    def __init__(self, n, rank, world, pview=False):
-        self.n, self.rank, self.world, self.pview = n, rank, world, pview
+    def __init__(self, n, rank, world, pview=False, rows=False):
+        self.n, self.rank, self.world, self.pview, self.rows = n, rank, world, pview, rows
         self.t = 0
 
     def step(self, k):
@@ -37,7 +38,7 @@ class FakeEngine:
                 "xgmi_bytes": 1000.0 * (self.rank + 1) * self.t}
 
     def digest(self, t):
-        if self.pview:                               # row shards: every rank counts its rows
+        if self.pview or self.rows:                  # row shards: every rank counts its rows
             rows = self.n // self.world
         else:
             rows = self.n if self.rank == 0 else 0
@@ -45,7 +46,7 @@ class FakeEngine:
                 "overflow": 0}
 
     def layout(self):
-        return (self.world, self.rank, self.n // self.world)
+        return (self.world, self.rank, self.n if self.rows else self.n // self.world)
 
     def close(self):
         pass
@@ -56,7 +57,8 @@ def _worker(rank, world, port, q):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import gossip_protocol_amd.dist as gd
-    gd.make_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world)
+    gd.make_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world,
+                                                          rows=kw.get("layout") == "rows")
     gd.make_pview_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world, pview=True)
     import bench
     buf = io.StringIO()
@@ -101,3 +103,12 @@ def test_bench_two_ranks_gloo():
         < 1e-6 * pv["value"]
     f = d["full262k"]
     assert f["config"]["nodes"] == 262144 and f["config"]["workload"].startswith("config4")
+    fr = d["full_rows"]
+    c3 = fr["config3"]
+    assert c3["config"]["parallelism"] == "rows2"
+    # row shards: whole rows (stride = n) of their own receivers, no slice factor
+    assert c3["roofline"]["algorithmic_bytes_per_launch"] == \
+        (2 * 512 + 2 * 512) * 2 * 1024 * 2 + 2 * 512 * 2 * 4
+    assert abs(c3["value"] - 1024 * min(N_STEPS, 8) / (c3["ms_per_step"] * min(N_STEPS, 8) / 1e3)) \
+        < 1e-6 * c3["value"]
+    assert "skipped" in fr["config4"]                 # does not fit 2 GPUs
