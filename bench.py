@@ -24,6 +24,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -271,6 +272,8 @@ def main(argv=None):
     ap.add_argument("--no-pview", action="store_true", help="skip the config-5 line item")
     ap.add_argument("--pview-nodes", type=int, default=PV_NODES)
     ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item (N > 1)")
+    ap.add_argument("--item-budget", type=int, default=420,
+                    help="seconds for the secondary line items before the line is printed as is")
     ap.add_argument("--no-rows", action="store_true",
                     help="skip the full-view row-layout line items (N > 1)")
     args = ap.parse_args(argv)
@@ -286,44 +289,67 @@ def main(argv=None):
             torch.cuda.set_device(local)
             dist.init_process_group("nccl")
     full = run_full(args.nodes, args.steps, args.warmup, world, local, dist)
-    pv = None
-    if not args.no_pview:
-        pv = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
-                       not args.no_cpu_baseline)
-    f262 = None
-    if world > 1 and not args.no_262k:
-        # BASELINE config 4: 262,144 nodes full view over the same column shards (its 137 GB
-        # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)
-        r = run_full(262144, min(args.steps, 8), 2, world, local, dist)
-        f262 = summarize_full(r, 262144, min(args.steps, 8), world)
-    rows = {}
-    if world > 1 and not args.no_rows:
-        # the full view ROW-sharded (north star: sender rows cross shards over RCCL send/recv,
-        # deduplicated per (sender, shard)); O(f n^2) xGMI bytes per tick against the column
-        # layout's O(n), reported beside it (DESIGN.md "Multi-GPU")
-        r = run_full(args.nodes, min(args.steps, 8), 2, world, local, dist, layout="rows")
-        rows["config3"] = summarize_full(r, args.nodes, min(args.steps, 8), world)
-        if not args.no_262k:
-            if world >= 4:
-                r = run_full(262144, 4, 2, world, local, dist, layout="rows")
-                rows["config4"] = summarize_full(r, 262144, 4, world)
-            else:
-                # 2 x 68.7 GB of table rows plus ~2 x 66 GB of send/receive rows per GPU
-                rows["config4"] = {"skipped": "row layout at 262,144 nodes needs > 270 GB per "
-                                              "GPU at N = 2 (tables + exchange regions)"}
-
+    out = None
     if rank == 0:
         out = summarize_full(full, args.nodes, args.steps, world)
         out.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                     "higher_is_better": True, "vs_baseline": None})
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
-        if pv is not None:
-            out["pview"] = pv
-        if f262 is not None:
-            out["full262k"] = f262
-        if rows:
-            out["full_rows"] = rows
+
+    # Secondary line items: an exception is recorded in the item (every rank sees the same
+    # deterministic capacity / allocation errors); a hang or a one-rank failure that stalls
+    # the others' collectives is cut by the watchdog, which prints the line as it stands.
+    done = threading.Event()
+
+    def _watchdog():
+        if done.wait(args.item_budget):
+            return
+        if out is not None:
+            out["incomplete"] = "secondary line items exceeded %d s" % args.item_budget
+            print(json.dumps(out), flush=True)
+        os._exit(0)
+    threading.Thread(target=_watchdog, daemon=True).start()
+
+    def item(key, fn, sub=None):
+        try:
+            res = fn()
+        except Exception as e:          # noqa: BLE001 -- reported, not swallowed
+            res = {"error": "%s: %s" % (type(e).__name__, e)}
+        if out is not None and res is not None:
+            if sub is None:
+                out[key] = res
+            else:
+                out.setdefault(key, {})[sub] = res
+
+    if not args.no_pview:
+        item("pview", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world,
+                                        local, dist, not args.no_cpu_baseline))
+    if world > 1 and not args.no_262k:
+        # BASELINE config 4: 262,144 nodes full view over the same column shards (its 137 GB
+        # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)
+        item("full262k", lambda: summarize_full(
+            run_full(262144, min(args.steps, 8), 2, world, local, dist), 262144,
+            min(args.steps, 8), world))
+    if world > 1 and not args.no_rows:
+        # the full view ROW-sharded (north star: sender rows cross shards over RCCL send/recv,
+        # deduplicated per (sender, shard)); O(f n^2) xGMI bytes per tick against the column
+        # layout's O(n), reported beside it (DESIGN.md "Multi-GPU")
+        item("full_rows", lambda: summarize_full(
+            run_full(args.nodes, min(args.steps, 8), 2, world, local, dist, layout="rows"),
+            args.nodes, min(args.steps, 8), world), "config3")
+        if not args.no_262k:
+            if world >= 4:
+                item("full_rows", lambda: summarize_full(
+                    run_full(262144, 4, 2, world, local, dist, layout="rows"), 262144, 4, world),
+                    "config4")
+            else:
+                # 2 x 68.7 GB of table rows plus ~2 x 66 GB of send/receive rows per GPU
+                item("full_rows", lambda: {"skipped": "row layout at 262,144 nodes needs > 270 GB "
+                                                      "per GPU at N = 2 (tables + exchange regions)"},
+                     "config4")
+    done.set()
+    if out is not None:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -8,9 +8,15 @@
 //   csr              received records -> deg, scan, local + remote scatter
 #include "rowx_host.hpp"
 
+#include <algorithm>
+
 #include "scale_kernels.hpp"
 
 namespace gsp {
+
+namespace {
+constexpr size_t kPiece = size_t(1) << 27;      // 8-byte words per ncclSend / ncclRecv (1 GiB)
+}
 
 hipError_t RowxBufs::alloc(int32_t shards, int64_t pair_cap, int64_t msg_cap, int32_t row_words,
                            int64_t csr_cap, hipStream_t st) {
@@ -90,15 +96,18 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
             if (h == me) continue;
             const size_t reg = size_t(rowx_region(h, me));      // same index for h's region here
             const size_t so = reg * size_t(job.pair_cap), mo = reg * size_t(job.msg_cap);
-            if (pairs(me, h))
-                GSP_NCCL(ncclSend(sh.x->send_rows.p + so * W, size_t(pairs(me, h)) * W, ncclUint64, h,
-                                  job.comm, st));
+            // full-view rows are 512 KB at 262,144 nodes: a region can pass 2^31 elements, so
+            // rows move in pieces of at most kPiece words (matched in order on both sides)
+            const size_t ns = size_t(pairs(me, h)) * W, nr = size_t(pairs(h, me)) * W;
+            for (size_t o = 0; o < ns; o += kPiece)
+                GSP_NCCL(ncclSend(sh.x->send_rows.p + so * W + o, std::min(kPiece, ns - o), ncclUint64,
+                                  h, job.comm, st));
             if (msgs(me, h))
                 GSP_NCCL(ncclSend(sh.x->send_rec.p + mo, size_t(msgs(me, h)) * 3, ncclInt32, h,
                                   job.comm, st));
-            if (pairs(h, me))
-                GSP_NCCL(ncclRecv(sh.x->recv_rows.p + so * W, size_t(pairs(h, me)) * W, ncclUint64, h,
-                                  job.comm, st));
+            for (size_t o = 0; o < nr; o += kPiece)
+                GSP_NCCL(ncclRecv(sh.x->recv_rows.p + so * W + o, std::min(kPiece, nr - o), ncclUint64,
+                                  h, job.comm, st));
             if (msgs(h, me))
                 GSP_NCCL(ncclRecv(sh.x->recv_rec.p + mo, size_t(msgs(h, me)) * 3, ncclInt32, h,
                                   job.comm, st));
