@@ -66,7 +66,7 @@ struct gsp_scale {
     int64_t stride = 0;        // columns per shard
     int32_t tick = 0;
     bool timing = true;
-    int policy = 1;            // bit 0 nt own row, bit 1 nt sender rows (A/B: profiles/r01)
+    int policy = 5;            // bit 0 nt own row, bit 1 nt sender rows, bit 2 pipelined loads
     int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
     std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
     std::vector<int32_t> h_fail;
@@ -103,6 +103,8 @@ struct gsp_scale {
         a.h0 = p.h0;
         a.nt_own = policy & 1;
         a.nt_src = (policy >> 1) & 1;
+        a.pipe = (policy >> 2) & 1;
+        a.tfail = p.tfail;
         a.count_rounds = rowmode || sh.g == 0;
         a.seed = p.seed;
         a.fail_tick = sh.fail_tick.p;
@@ -172,6 +174,8 @@ int validate_scale_params(const gsp_scale_params *p) {
     GSP_REQUIRE(p->h0 >= 1 && p->h0 < 2047, GSP_ERR_INVALID, "h0=%d outside [1,2046]", p->h0);
     GSP_REQUIRE(p->drop_pct >= 0 && p->drop_pct <= 100, GSP_ERR_INVALID, "drop_pct=%d", p->drop_pct);
     GSP_REQUIRE(p->fail_mode >= 0 && p->fail_mode <= 2, GSP_ERR_INVALID, "fail_mode=%d", p->fail_mode);
+    GSP_REQUIRE(p->tfail == 0 || (p->tfail >= 1 && p->tfail < p->tremove), GSP_ERR_INVALID,
+                "tfail=%d: 0 (off) or 1..tremove-1", p->tfail);
     GSP_REQUIRE(p->max_ticks >= 1 && int64_t(p->h0) + p->max_ticks <= 2047, GSP_ERR_RANGE,
                 "h0 + max_ticks = %d exceeds the 11-bit packed heartbeat (2047)",
                 p->h0 + p->max_ticks);
@@ -371,7 +375,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                                        int64_t(double(rows_max) * p->fanout / shards * 1.25) + 4096);
     }
     s->h_fail = gsp::scale_fail_ticks(*p);
-    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 3;
+    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 7;
     if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
     if (!s->sliced) {
         // the fused kernel keeps the row's presence bitmap in LDS next to 8.3 KB of statics
@@ -634,7 +638,7 @@ int gsp_scale_set_timing(gsp_scale *s, int32_t on) {
 }
 
 int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy) {
-    GSP_REQUIRE(s && policy >= 0 && policy <= 3, GSP_ERR_INVALID,
+    GSP_REQUIRE(s && policy >= 0 && policy <= 7, GSP_ERR_INVALID,
                 "gsp_scale_set_cache_policy: policy %d", policy);
     s->policy = policy;
     return GSP_OK;

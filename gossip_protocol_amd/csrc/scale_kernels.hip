@@ -190,8 +190,12 @@ __device__ inline int32_t next_distinct_rank(uint32_t u, int32_t cnt, int32_t k,
     return rk;
 }
 
-// kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads
-template <bool kInit, bool kSlice, int kMerge, int kPolicy>
+// kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads.
+// kPipe: software-pipelined chunk loads (the next chunk is requested before this one merges).
+// kTfail: TFAIL suspicion (a.tfail > 0): a sender's payload holds only the members it could
+// gossip at send time (t - 1 - ts < tfail), and only members with t - ts < tfail get a
+// presence bit (peer choice) and count.
+template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe = false, bool kTfail = false>
 __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
     constexpr bool kNtOwn = (kPolicy & 1) != 0, kNtSrc = (kPolicy & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // fused: stride/32 words
@@ -247,11 +251,40 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     const uint32_t t5 = uint32_t(t) & 31u;
     const uint32_t tr = uint32_t(a.tremove);
     const PackedConsts pc = packed_consts(t5, tr);
+    const uint32_t tf = uint32_t(a.tfail);
+    const uint32_t tfx2 = tf | (tf << 16);
+    const uint32_t t5m1 = uint32_t(t - 1) & 31u;                  // the senders' tick, mod 32
+    const uint32_t t32m1 = (t5m1 | (t5m1 << 16)) + 0x00200020u;
+    // kTfail: drop the payload entries the sender had suspected when it sent (packed pair)
+    auto gossiped = [&](uint32_t w) -> uint32_t {
+        const uint32_t age = (t32m1 - (w & pc.low5)) & pc.low5;
+        return w & pk_sub(pc.zero, pk_min(pk_subc(tfx2, age), pc.one));
+    };
     const int64_t stride = a.stride;
     const uint16_t *own_prev = a.prev + int64_t(lr) * stride;
     uint16_t *own_cur = a.cur + int64_t(lr) * stride;
     uint32_t live = 0, joins = 0, removes = 0;
     uint64_t hsum = 0;
+
+    // kPipe: the first 4 sender rows as wave-uniform (scalar) pointers, and the request of one
+    // chunk's own + sender vectors (16 B per lane each) issued one chunk ahead
+    const uint16_t *srow[4];
+    uint4 pe = make_uint4(0u, 0u, 0u, 0u), pv[4];
+    auto issue = [&](int64_t col) {
+        pe = ld16<kNtOwn>(own_prev + col);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (u < k) pv[u] = ld16<kNtSrc>(srow[u] + col);
+    };
+    if (kPipe && !kInit) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            pv[u] = make_uint4(0u, 0u, 0u, 0u);
+            const int32_t sl = __builtin_amdgcn_readfirstlane(u < k ? s_slot[u] : 0);
+            srow[u] = sl >= 0 ? a.prev + int64_t(sl) * stride : a.remote + int64_t(-sl - 1) * stride;
+        }
+        issue(int64_t(tid) * kEntriesPerLane);
+    }
 
     for (int64_t c0 = 0; c0 < stride; c0 += kChunk) {
         const int64_t lc0 = c0 + int64_t(tid) * kEntriesPerLane;   // column in this table
@@ -268,22 +301,44 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                 ws[i] = lo | (hi << 16);
             }
         } else {
-            uint4 e = ld16<kNtOwn>(own_prev + lc0);
+            uint4 e;
+            uint4 cv[4];
+            if (kPipe) {
+                // chunk c's own and first 4 sender vectors arrived with the previous request;
+                // chunk c + 1's are requested before chunk c is merged
+                e = pe;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cv[u] = pv[u];
+                if (c0 + kChunk < stride) issue(lc0 + kChunk);
+            } else {
+                e = ld16<kNtOwn>(own_prev + lc0);
+            }
             w0[0] = e.x; w0[1] = e.y; w0[2] = e.z; w0[3] = e.w;
             for (int32_t j0 = 0; j0 < k; j0 += 4) {
                 uint4 v[4];
+                if (kPipe && j0 == 0) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (j0 + u < k) {
-                        const int32_t sl = s_slot[j0 + u];
-                        const uint16_t *row = sl >= 0 ? a.prev + int64_t(sl) * stride
-                                                      : a.remote + int64_t(-sl - 1) * stride;
-                        v[u] = ld16<kNtSrc>(row + lc0);
+                    for (int u = 0; u < 4; ++u) v[u] = cv[u];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (j0 + u < k) {
+                            const int32_t sl = s_slot[j0 + u];
+                            const uint16_t *row = sl >= 0 ? a.prev + int64_t(sl) * stride
+                                                          : a.remote + int64_t(-sl - 1) * stride;
+                            v[u] = ld16<kNtSrc>(row + lc0);
+                        }
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (j0 + u >= k) break;
+                    if (kTfail) {
+                        v[u].x = gossiped(v[u].x);
+                        v[u].y = gossiped(v[u].y);
+                        v[u].z = gossiped(v[u].z);
+                        v[u].w = gossiped(v[u].w);
+                    }
                     if (kMerge == 1) {
                         e.x = merge_word_packed(e.x, v[u].x, pc);
                         e.y = merge_word_packed(e.y, v[u].y, pc);
@@ -318,7 +373,8 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                 const uint32_t age = (pc.t32 - (ws[i] & pc.low5)) & pc.low5;
                 ev |= pk_min(pk_subc(age, pc.trm1), pe);          // present and stale
                 ev |= pk_subc(pe, pk_min(w0[i], pc.one));          // absent before, present now
-                q |= ((pe | (pe >> 15)) & 3u) << (2 * i);
+                const uint32_t pg = kTfail ? pk_min(pe, pk_min(pk_subc(tfx2, age), pc.one)) : pe;
+                q |= ((pg | (pg >> 15)) & 3u) << (2 * i);
             }
             slow = ev != 0;
             bits = q;
@@ -341,7 +397,8 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                         hsum += event_mix(1, uint32_t(t), uint32_t(r), uint32_t(gc0 + i));
                     }
                 }
-                bits |= (ent ? 1u : 0u) << i;
+                const bool counted = ent && (!kTfail || ((t5 - ent) & 31u) < tf);
+                bits |= (counted ? 1u : 0u) << i;
             }
         }
         live += __builtin_popcount(bits);
@@ -598,6 +655,14 @@ hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st)
 template <bool kSlice, int kMerge>
 void launch_tick_policy(const ScaleTickArgs &a, int policy, size_t lds, hipStream_t st) {
     const dim3 grid(a.rows), block(kScaleBlock);
+    if (a.tfail > 0) {
+        hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, false, true>), grid, block, lds, st, a);
+        return;
+    }
+    if (a.pipe && kMerge == 1 && (policy & 3) == 1) {
+        hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, true>), grid, block, lds, st, a);
+        return;
+    }
     switch (policy & 3) {
         case 0: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 0>), grid, block, lds, st, a); break;
         case 1: hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1>), grid, block, lds, st, a); break;

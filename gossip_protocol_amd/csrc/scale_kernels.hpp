@@ -40,6 +40,9 @@ struct ScaleTickArgs {
     int32_t drop_pct;
     int32_t h0;
     int32_t nt_own, nt_src;      // non-temporal policy of the own-row / sender-row streams
+    int32_t pipe;                // software-pipelined chunk loads (packed merge, policy 1)
+    int32_t tfail;               // TFAIL suspicion: 0 off, else members this stale are not
+                                 // gossiped / chosen / counted
     int32_t count_rounds;        // this shard adds node-rounds / merges / sends to the digest
     uint64_t seed;
     const int32_t *fail_tick;    // [n] global

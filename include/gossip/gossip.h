@@ -193,6 +193,10 @@ typedef struct {
     int32_t fail_ppm;   /* failure fraction in parts per million                       */
     uint64_t seed;
     int32_t max_ticks;  /* bound for digest storage; hb must stay <= 2047 (h0+ticks)   */
+    int32_t tfail;      /* TFAIL suspicion (MP1Node.h:22, unused by the reference): 0 off;
+                           1..tremove-1: a member whose heartbeat is tfail or more ticks
+                           old is suspected -- listed until TREMOVE but not gossiped, not
+                           chosen as a peer and not counted (DESIGN.md "Scale mode")   */
 } gsp_scale_params;
 
 typedef struct {
@@ -264,7 +268,8 @@ int gsp_scale_perf_get(gsp_scale *s, gsp_scale_perf *out);
 /* Enable/disable per-launch HIP event timing (default on). */
 int gsp_scale_set_timing(gsp_scale *s, int32_t on);
 /* Cache policy of the row streams of the fused tick kernel: bit 0 = non-temporal loads
- * and stores of the receiver's own row, bit 1 = non-temporal loads of sender rows.
+ * and stores of the receiver's own row, bit 1 = non-temporal loads of sender rows, bit 2 =
+ * software-pipelined chunk loads (with bit 0 and the packed merge; default 5).
  * Results are identical for every policy; only speed differs. */
 int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy);
 /* Merge arithmetic: 1 = packed 16-bit (two entries per v_pk_* instruction, default),

@@ -46,6 +46,9 @@ typedef struct {
     int32_t fail_tick;  /* nodes fail at the end of this tick               */
     int32_t fail_ppm;   /* failure fraction, parts per million              */
     uint64_t seed;
+    int32_t tfail;      /* 0: off (the reference: TFAIL unused); else members with
+                           t - ts >= tfail are suspected: not gossiped, not chosen as
+                           peers, not counted (MP1Node.h:22, spec p.3)         */
 } gsp_scale_cfg;
 
 typedef struct {

@@ -12,7 +12,11 @@
  * What the reference leaves undefined at scale (it asserts N <= 1000, EmulNet.h:10, and
  * filters ids >= 10, MP1Node.cpp:245) is fixed by the build: pre-joined start, no id
  * filter, receipt in ascending sender order, Philox peer choice (fanout f, distinct
- * peers) and Philox drop/failure draws.  The GPU engine stores entries packed
+ * peers) and Philox drop/failure draws.
+ * TFAIL suspicion (the reference defines TFAIL = 5, MP1Node.h:22, and never
+ * uses it): with cfg.tfail > 0 a member whose heartbeat is tfail or more ticks old is
+ * SUSPECTED -- still listed until TREMOVE, but left out of the payload a node gossips, of its
+ * peer choice and of its member count.  The GPU engine stores entries packed
  * (hb:11 | ts mod 32:5); this restatement keeps absolute values so that parity tests
  * prove the packing loses nothing observable.
  */
@@ -44,6 +48,11 @@ uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
 
 static int alive_at(const gsp_scale_oracle *o, int32_t r, int32_t t) { return t <= o->fail_tick[r]; }
 
+/* a listed member with timestamp ts is gossiped / chosen / counted at tick t */
+static int gossipable(const gsp_scale_cfg *c, int32_t t, int32_t ts) {
+    return c->tfail <= 0 || t - ts < c->tfail;
+}
+
 static void compute_fail_ticks(gsp_scale_oracle *o) {
     const gsp_scale_cfg *c = &o->c;
     for (int32_t r = 0; r < c->n; ++r) o->fail_tick[r] = 0x7FFFFFFF;
@@ -69,6 +78,7 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
     for (int32_t s = 0; s < n; ++s) {
         if (!alive_at(o, s, t)) continue;
         const uint8_t *ps = o->pres[tab] + (size_t)s * n;
+        const int32_t *tss = o->ts[tab] + (size_t)s * n;
         int32_t cnt = o->cnt[s];
         int32_t keff = c->fanout < cnt ? c->fanout : cnt;
         int32_t nch = 0;
@@ -81,10 +91,10 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
             memmove(&chosen[pos + 1], &chosen[pos], sizeof(int32_t) * (nch - pos));
             chosen[pos] = rk;
             nch++;
-            /* rank -> column: rk-th present column in ascending order */
+            /* rank -> column: rk-th gossipable column in ascending order */
             int32_t seen = -1, dst = -1;
             for (int32_t x = 0; x < n; ++x)
-                if (ps[x] && ++seen == rk) { dst = x; break; }
+                if (ps[x] && gossipable(c, t, tss[x]) && ++seen == rk) { dst = x; break; }
             if (d) d->sent++;
             uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, (uint32_t)s,
                                          (uint32_t)dst, 3u);
@@ -193,7 +203,8 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
                 d->joins++; d->event_hash += gsp_event_mix(1, t, r, s);
             }
             for (int32_t x = 0; x < n; ++x) {
-                if (!Ps[x] || x == s) continue;
+                /* the payload: s's members gossipable when s sent it (tick t - 1) */
+                if (!Ps[x] || x == s || !gossipable(c, t - 1, Ss[x])) continue;
                 if (P[x]) {
                     if (Hs[x] > H[x]) { H[x] = Hs[x]; S[x] = t; }
                 } else if (x != r && t - Ss[x] < T) {
@@ -210,7 +221,7 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
                 P[x] = 0; H[x] = 0; S[x] = 0;
                 d->removes++; d->event_hash += gsp_event_mix(2, t, r, x);
             } else {
-                live++;
+                live += gossipable(c, t, S[x]);
             }
         }
         cnt_next[r] = live;

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine  # noqa: E402
 
 VARIANTS = [("scalar", 0, 0), ("scalar", 0, 1), ("packed", 1, 0), ("packed", 1, 1),
-            ("packed", 1, 3)]
+            ("packed", 1, 3), ("packed", 1, 5)]     # policy bit 2: pipelined chunk loads
 
 
 def main():

@@ -46,12 +46,16 @@ VARIANTS = {
     "rows2": (2, "rows", 1, 1),
     "rows3": (3, "rows", 1, 1),
     "rows8_scalar": (8, "rows", 0, 2),
+    "fused_pipe": (1, "columns", 1, 5),
+    "rows3_pipe": (3, "rows", 1, 5),
+    "columns2_pipe": (2, "columns", 1, 5),
 }
 VARIANT_CASES = [(c, "fused") for c in CASES] + [
     (CASES[1], "fused_scalar_merge"), (CASES[3], "fused_nt_all"), (CASES[1], "columns2"),
     (CASES[3], "columns3"), (CASES[4], "columns2"), (CASES[2], "columns4_scalar"),
     (CASES[0], "rows2"), (CASES[1], "rows3"), (CASES[3], "rows2"), (CASES[4], "rows3"),
-    (CASES[2], "rows8_scalar")]
+    (CASES[2], "rows8_scalar"), (CASES[3], "fused_pipe"), (CASES[4], "fused_pipe"),
+    (CASES[1], "rows3_pipe"), (CASES[3], "columns2_pipe")]
 
 
 @pytest.mark.parametrize("case,variant", VARIANT_CASES,
@@ -88,6 +92,48 @@ def test_scale_matches_oracle(case, variant):
         assert perf["ticks"] == ticks and perf["merge_ms"] > 0
         if layout == "rows" and group > 1:
             assert perf["xgmi_bytes"] > 0
+
+
+TFAIL_CASES = [
+    # (case, shards, layout, merge, tfail): TFAIL suspicion, the reference's
+    # TFAIL = 5 (MP1Node.h:22) and a few others
+    (CASES[2], 1, "columns", 1, 5),
+    (CASES[1], 1, "columns", 0, 5),
+    (CASES[3], 1, "columns", 1, 3),
+    (CASES[4], 1, "columns", 1, 12),
+    (CASES[1], 2, "columns", 1, 5),
+    (CASES[3], 3, "rows", 1, 5),
+]
+
+
+@pytest.mark.parametrize("case,shards,layout,merge,tfail", TFAIL_CASES,
+                         ids=lambda x: "n%d_f%d_d%d_m%d" % x[:4] if isinstance(x, tuple) else str(x))
+def test_tfail_matches_oracle(case, shards, layout, merge, tfail):
+    """TFAIL suspicion: members tfail or more ticks stale are listed but neither gossiped nor
+    chosen as peers nor counted.  Digests every tick, messages and rows vs the oracle."""
+    n, f, drop, mode, ftick, ppm, seed, ticks = case
+    orc = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                      seed=seed, tfail=tfail)
+    plain = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+                        fail_ppm=ppm, seed=seed)
+    differs = False
+    with ScaleEngine(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                     seed=seed, max_ticks=ticks, group=shards, layout=layout, tfail=tfail) as eng:
+        eng.set_merge(merge)
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            differs |= want != plain.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d" % t
+            if t % 9 == 0 or t == ticks:
+                src, dst = orc.messages()
+                m = eng.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+        _compare_state(eng, orc, n, range(0, n, 7))
+    assert differs, "suspicion changed nothing: the case does not exercise TFAIL"
+    orc.close()
+    plain.close()
 
 
 def test_rccl_rank_path_one_rank():
