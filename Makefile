@@ -23,7 +23,7 @@ OBJS     := $(patsubst $(CSRC)/%.hip,build/%.hip.o,$(KERNELS)) \
             $(patsubst $(CSRC)/%.cpp,build/%.cpp.o,$(HOSTSRC))
 HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard include/gossip/*.h) $(wildcard include/gossip/*.hpp)
 
-.PHONY: all lib app oracle clean
+.PHONY: all lib app oracle clean lib-variant
 all: lib app oracle
 
 lib: $(LIB)
@@ -49,6 +49,14 @@ $(APP): $(PKG)/app/app_main.cpp $(LIB) include/gossip/mp1_facade.hpp
 oracle:
 	$(MAKE) -C oracle
 
+# kernel A/B variant: make lib-variant TAG=x VFLAGS=-DGSP_...  ->  $(PKG)/libgossip_amd.x.so
+# (loaded with GSP_LIB_VARIANT=x; experiments only, the product is $(LIB))
+lib-variant: $(KERNELS) $(HOSTSRC) $(HDRS)
+	mkdir -p build/v-$(TAG)
+	for f in $(KERNELS) $(HOSTSRC); do \
+	  $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o build/v-$(TAG)/$$(basename $$f).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -o $(PKG)/libgossip_amd.$(TAG).so build/v-$(TAG)/*.o $(LDFLAGS)
+
 clean:
-	rm -rf build $(LIB) $(PKG)/bin
+	rm -rf build $(LIB) $(PKG)/libgossip_amd.*.so $(PKG)/bin
 	$(MAKE) -C oracle clean

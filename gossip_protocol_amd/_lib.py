@@ -9,6 +9,10 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgossip_amd.so")
+# kernel A/B experiments (scripts/ab_*.py): GSP_LIB_VARIANT=<tag> loads the in-tree
+# libgossip_amd.<tag>.so built by `make lib-variant`
+if os.environ.get("GSP_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_HERE, "libgossip_amd.%s.so" % os.environ["GSP_LIB_VARIANT"])
 
 c_int32 = ctypes.c_int32
 c_int64 = ctypes.c_int64

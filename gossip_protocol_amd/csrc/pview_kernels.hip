@@ -39,13 +39,27 @@ constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: abov
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
 static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
 
-__device__ inline uint64_t pv_event_mix(uint32_t kind, uint32_t t, uint32_t r, uint32_t x) {
-    uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) |
-                 (uint64_t(r & 0x1FFFFF) << 21) | uint64_t(x & 0x1FFFFF);
+// Event digest term (oracle/pview_oracle.c gsp_pv_event_mix): a row seed per kind (1 join,
+// 2 remove, 3 evict), computed once per row, and a three-multiply finaliser of the member id
+// per event (a row hashes ~1000 events per tick).
+__device__ inline uint64_t pv_seed(uint32_t kind, uint32_t t, uint32_t r) {
+    uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) | (uint64_t(r & 0x1FFFFF) << 21);
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+__device__ inline uint64_t pv_hash(uint64_t S, uint32_t x) {
+#ifdef GSP_PV_EXP_NOHASH
+    return 0;
+#endif
+    uint32_t a = (x ^ uint32_t(S)) * 0x9E3779B1u;
+    a ^= a >> 16;
+    a *= 0x85EBCA6Bu;
+    a ^= a >> 13;
+    uint32_t b = a * 0xC2B2AE35u;
+    b ^= b >> 16;
+    return S + ((uint64_t(b) << 32) | a);
 }
 
 // the reference's merge of one payload entry (packed hb << 5 | ts5, 0 = absent)
@@ -182,11 +196,14 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                                              const int32_t (&sslot)[kPvMaxInbox], RowOut &ro,
                                              PvMark &pm) {
     constexpr int Q = kBlocks;                           // keys per lane
+    constexpr int kJ = kBlocks - 1;                      // k <= kJ messages in this variant
     constexpr int P = kBlocks * kSlots;
     const int32_t tid = threadIdx.x;
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
     const int32_t Pe = (k + 1) * kSlots;                // keys that can be real
+    const uint64_t S_join = pv_seed(1, t, uint32_t(r)), S_remove = pv_seed(2, t, uint32_t(r)),
+                   S_evict = pv_seed(3, t, uint32_t(r));
 
     // ---- 2. keys: one sorted block of 256 slots per source -----------------------------------
     uint64_t ent[kBlocks];
@@ -283,7 +300,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             av = ae0 = 0;
             ajs = 0;
 #pragma unroll
-            for (int jj = 0; jj < kPvMaxInbox; ++jj) ajs = ssrc[jj] == x ? uint32_t(jj + 1) : ajs;
+            for (int jj = 0; jj < kJ; ++jj) ajs = ssrc[jj] == x ? uint32_t(jj + 1) : ajs;
             adone = false;
             if (aown && ajs) found_mask |= 1u << (ajs - 1);
         }
@@ -311,10 +328,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (!aown) continue;
         if (ajs && !adone) av = pv_event(av, t5);
         if (x == uint32_t(r) || !av) continue;                  // never list yourself
-        if (!ae0) { joins++; hsum += pv_event_mix(1, t, uint32_t(r), x); }
+        if (!ae0) { joins++; hsum += pv_hash(S_join, x); }
         if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
-            hsum += pv_event_mix(2, t, uint32_t(r), x);
+            hsum += pv_hash(S_remove, x);
             continue;
         }
         res[e] = av;
@@ -325,7 +342,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     uint32_t adopt = 0;
     int32_t ains[kPvMaxInbox];
 #pragma unroll
-    for (int jj = 0; jj < kPvMaxInbox; ++jj) {
+    for (int jj = 0; jj < kJ; ++jj) {
         ains[jj] = 0;
         const uint32_t x = ssrc[jj];
         if (jj < k && x >= lo_id && x <= hi_id && beg <= Pe && !((found_mask >> jj) & 1u)) {
@@ -336,7 +353,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             adopt |= 1u << jj;
             nloc++;
             joins++;
-            hsum += pv_event_mix(1, t, uint32_t(r), x);
+            hsum += pv_hash(S_join, x);
         }
     }
 
@@ -352,7 +369,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     int32_t o_p = -1;
     if (n_orph == 1) {
 #pragma unroll
-        for (int jj = 0; jj < kPvMaxInbox; ++jj)
+        for (int jj = 0; jj < kJ; ++jj)
             if ((adopt >> jj) & 1u) { o_x = ssrc[jj]; o_p = ains[jj]; }
     }
     const bool multi = __ballot(n_orph > 1) != 0ull;          // wave-uniform
@@ -366,8 +383,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         } else {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
+#ifdef GSP_PV_MULTI_LOOP
+#pragma unroll 1
+#else
 #pragma unroll
-                for (int jj = 0; jj < kPvMaxInbox; ++jj)
+#endif
+                for (int jj = 0; jj < kJ; ++jj)
                     if (((adopt >> jj) & 1u) && ains[jj] == e) f(fresh, ssrc[jj]);
                 if (e < Q && res[e]) f(res[e], rid[e]);
             }
@@ -483,7 +504,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 w++;
             } else {
                 evicts++;
-                hsum += pv_event_mix(3, t, uint32_t(r), x);
+                hsum += pv_hash(S_evict, x);
             }
         });
         ro.ids_off = lds_word(sh, Wid);
@@ -601,8 +622,12 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
             sslot[jj] = __builtin_amdgcn_readlane(my_slot, jj);
         }
         pm.mark(0);
+#ifdef GSP_PV_FEWVAR
+        if (k <= 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+#else
         if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+#endif
         else if (k <= 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else pv_merge_row<8>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         pm.mark(5);

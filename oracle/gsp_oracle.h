@@ -78,6 +78,7 @@ int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32
                                   int64_t cap);
 
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x);
+uint64_t gsp_pv_event_mix(int kind, int64_t t, int64_t r, int64_t x);   /* partial view */
 
 /* ---- partial-view scale protocol restatement (pview_oracle.c) ---- */
 typedef struct {

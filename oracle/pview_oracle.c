@@ -35,6 +35,20 @@ struct gsp_pview_oracle {
 
 static int alive_at(const gsp_pview_oracle *o, int32_t r, int32_t t) { return t <= o->fail_tick[r]; }
 
+/* Event digest term of the partial view (kinds: 1 join, 2 remove, 3 evict).  A row seed
+ * S = gsp_event_mix(kind, t, r, 0) and a three-multiply 32-bit finaliser of the member id:
+ * the kernel hashes ~1000 events per row per tick, so the per-event part stays cheap. */
+uint64_t gsp_pv_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
+    const uint64_t S = gsp_event_mix(kind, t, r, 0);
+    uint32_t a = ((uint32_t)x ^ (uint32_t)S) * 0x9E3779B1u;
+    a ^= a >> 16;
+    a *= 0x85EBCA6Bu;
+    a ^= a >> 13;
+    uint32_t b = a * 0xC2B2AE35u;
+    b ^= b >> 16;
+    return S + (((uint64_t)b << 32) | a);
+}
+
 static void pv_fail_ticks(gsp_pview_oracle *o) {
     const gsp_pview_cfg *c = &o->c;
     for (int32_t r = 0; r < c->n; ++r) o->fail_tick[r] = 0x7FFFFFFF;
@@ -232,9 +246,9 @@ int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
                 }
             }
             if (!present) continue;
-            if (!e0) { d->joins++; d->event_hash += gsp_event_mix(1, t, r, x); }
+            if (!e0) { d->joins++; d->event_hash += gsp_pv_event_mix(1, t, r, x); }
             if (t - cur.ts >= T) {                              /* MP1Node.cpp:340 */
-                d->removes++; d->event_hash += gsp_event_mix(2, t, r, x);
+                d->removes++; d->event_hash += gsp_pv_event_mix(2, t, r, x);
                 continue;
             }
             res[nres++] = cur;
@@ -245,7 +259,7 @@ int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
             qsort(kk, nres, sizeof(keyed), cmp_keep);
             for (int32_t i = V; i < nres; ++i) {
                 d->evicts++;
-                d->event_hash += gsp_event_mix(3, t, r, kk[i].e.id);
+                d->event_hash += gsp_pv_event_mix(3, t, r, kk[i].e.id);
             }
             for (int32_t i = 0; i < V; ++i) res[i] = kk[i].e;
             nres = V;
