@@ -570,6 +570,14 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
     // the own view is requested before anything else (its latency overlaps the record's)
     const uint64_t ent0 = (!kInit && tid < V) ? __builtin_nontemporal_load(a.prev + int64_t(lr) * V + tid)
                                               : kPvEmpty;
+    // the receipt record (pview_receipt_kernel) is requested next, before the liveness test,
+    // so the three loads' latencies overlap
+    int32_t info = 0, my_src = 0, my_slot = 0;
+    if constexpr (!kInit) {
+        info = a.rc_info[lr];
+        my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
+        my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
+    }
     if (a.tick > a.fail_tick[r]) {          // crashed: no recv, no ops, no send
         if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
         return;
@@ -604,16 +612,13 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
         ro.vals_off = lds_half(sh, sh.vals);
         __syncthreads();
     } else {
-        // ---- 1. receipt record (pview_receipt_kernel), read by every wave --------------------
-        const int32_t info = a.rc_info[lr];
+        // ---- 1. receipt record (loaded above), read by every wave -----------------------------
         k = info & 7;
         k_all = info >> 3;
         if (k_all > kPvMaxSegment) {        // flagged by the receipt kernel
             if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
             return;
         }
-        const int32_t my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
-        const int32_t my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
         uint32_t ssrc[kPvMaxInbox];
         int32_t sslot[kPvMaxInbox];
 #pragma unroll
