@@ -153,12 +153,25 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "merges_per_s": merges / el,
         "xgmi_bytes_per_tick": xgmi, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": None, "kernel": "pview_tick_kernel",
+                     "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
+                     "kernel": "pview_tick_kernel",
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
     }
     if world == 1 and cpu_baseline_on:
         out["cpu_baseline"] = pview_cpu_baseline()
     return out
+
+
+def _pview_traffic(nodes, world):
+    """HBM bytes per tick-kernel launch from the committed PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, scripts/pmc_traffic.py --pview) for the one-GPU config-5 run, else None."""
+    prof = os.path.join(ROOT, "profiles", "pmc_traffic_pview.json")
+    if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
+        return None
+    try:
+        return json.load(open(prof)).get("bytes_per_launch")
+    except Exception:
+        return None
 
 
 def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):

@@ -110,32 +110,40 @@ __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_w
     return incl - v + before;
 }
 
+// N consecutive words at p: 16-B accesses when N % 4 == 0, 8-B when N % 2 == 0 (p is then
+// 8-B aligned: word offset lane * N), else single words
 template <int N>
 __device__ inline void lds_store(uint32_t *p, const uint32_t (&v)[N]) {
-    if constexpr (N == 1) {
-        p[0] = v[0];
-    } else if constexpr (N == 2) {
-        *reinterpret_cast<uint2 *>(p) = make_uint2(v[0], v[1]);
-    } else {
+    if constexpr (N % 4 == 0) {
 #pragma unroll
         for (int i = 0; i < N; i += 4)
             *reinterpret_cast<uint4 *>(p + i) = make_uint4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+    } else if constexpr (N % 2 == 0) {
+#pragma unroll
+        for (int i = 0; i < N; i += 2) *reinterpret_cast<uint2 *>(p + i) = make_uint2(v[i], v[i + 1]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) p[i] = v[i];
     }
 }
 
 template <int N>
 __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
-    if constexpr (N == 1) {
-        v[0] = p[0];
-    } else if constexpr (N == 2) {
-        const uint2 x = *reinterpret_cast<const uint2 *>(p);
-        v[0] = x.x; v[1] = x.y;
-    } else {
+    if constexpr (N % 4 == 0) {
 #pragma unroll
         for (int i = 0; i < N; i += 4) {
             const uint4 x = *reinterpret_cast<const uint4 *>(p + i);
             v[i] = x.x; v[i + 1] = x.y; v[i + 2] = x.z; v[i + 3] = x.w;
         }
+    } else if constexpr (N % 2 == 0) {
+#pragma unroll
+        for (int i = 0; i < N; i += 2) {
+            const uint2 x = *reinterpret_cast<const uint2 *>(p + i);
+            v[i] = x.x; v[i + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = p[i];
     }
 }
 
@@ -187,7 +195,7 @@ struct RowOut {
     uint64_t hsum;
 };
 
-// Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 4 or 8).
+// Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
 template <int kBlocks>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
@@ -231,39 +239,51 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
-    const int32_t beg = tid * Q;
+    // Level s merges neighbouring segments of s keys (the last one of a level may be shorter
+    // or alone when kBlocks is not a power of two).  The tree hands out Qt = 2^ceil(log2 Q)
+    // outputs per lane, so a lane's outputs never straddle two merges (P / Qt lanes work).
+    constexpr int Qt = Q <= 2 ? Q : Q <= 4 ? 4 : 8;
+    constexpr bool kPow2 = (kBlocks & (kBlocks - 1)) == 0;
+    const int32_t begt = tid * Qt;
     int cur = 0;
 #pragma unroll
     for (int s = kSlots; s < P; s <<= 1) {
-        if (beg < Pe) {
+        if (begt < Pe) {
             const uint32_t *X = sh.keys[cur];
             uint32_t *Y = sh.keys[cur ^ 1];
-            const int32_t b = beg / (2 * s), o = beg - b * 2 * s;
+            const int32_t b = begt / (2 * s), o = begt - b * 2 * s;
             const uint32_t *A = X + b * 2 * s, *B = A + s;
-            int32_t lo = o > s ? o - s : 0, hi = o < s ? o : s;
+            int32_t sa = s, sb = s;
+            if constexpr (!kPow2) {
+                const int32_t rest = P - b * 2 * s;
+                sa = rest < s ? rest : s;
+                sb = rest - s < s ? (rest > s ? rest - s : 0) : s;
+            }
+            int32_t lo = o > sb ? o - sb : 0, hi = o < sa ? o : sa;
             while (lo < hi) {                                  // co-rank of output o
                 const int32_t mid = (lo + hi) >> 1;
                 if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
             }
             int32_t i = lo, j = o - lo;
-            uint32_t va = i < s ? A[i] : kKeyMax, vb = j < s ? B[j] : kKeyMax;
-            uint32_t outk[Q];
+            uint32_t va = i < sa ? A[i] : kKeyMax, vb = j < sb ? B[j] : kKeyMax;
+            uint32_t outk[Qt];
 #pragma unroll
-            for (int e = 0; e < Q; ++e) {
+            for (int e = 0; e < Qt; ++e) {
                 const bool ta = va <= vb;                      // equal only for padding
                 outk[e] = ta ? va : vb;
                 i += ta ? 1 : 0;
                 j += ta ? 0 : 1;
                 const int32_t ii = ta ? i : j;
-                const uint32_t nv = ii < s ? (ta ? A : B)[ii] : kKeyMax;
+                const uint32_t nv = ii < (ta ? sa : sb) ? (ta ? A : B)[ii] : kKeyMax;
                 va = ta ? nv : va;
                 vb = ta ? vb : nv;
             }
-            lds_store<Q>(Y + beg, outk);
+            lds_store<Qt>(Y + begt, outk);
         }
         __syncthreads();
         cur ^= 1;
     }
+    const int32_t beg = tid * Q;                               // the fold's Q keys per lane
     const uint32_t *C = sh.keys[cur];
     uint32_t *const age_hist = sh.keys[cur ^ 1];              // dead after the tree
     uint32_t *const scan_buf = sh.keys[cur ^ 1] + 2040;
@@ -627,13 +647,12 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
             sslot[jj] = __builtin_amdgcn_readlane(my_slot, jj);
         }
         pm.mark(0);
-#ifdef GSP_PV_FEWVAR
-        if (k <= 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-#else
+        // one variant per key count (own view + k sender views), k = 4, 5 and 6, 7 sharing
         if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-#endif
-        else if (k <= 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k == 2) pv_merge_row<3>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k == 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k <= 5) pv_merge_row<6>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else pv_merge_row<8>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         pm.mark(5);
     }

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of the fused tick kernel from rocprofv3 PMC passes.
 
-    python scripts/pmc_traffic.py <pmc_fetch.csv> <pmc_write.csv> [out.json]
+    python scripts/pmc_traffic.py <pmc_fetch.csv> <pmc_write.csv> [out.json] [--pview]
+
+--pview: the partial-view tick kernel (8-B/lane view loads and stores) instead of the
+full-view fused tick kernel.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts half of
 the bytes of a wide (16 B/lane) coalesced streaming read, which is every load of this
@@ -13,6 +16,7 @@ import json
 import sys
 
 KERNEL = "scale_tick_kernel<false"
+NOTE = "FETCH_SIZE x2 (gfx950 counts half of 16-B/lane streaming reads)"
 
 
 def per_launch(path, counter):
@@ -22,17 +26,25 @@ def per_launch(path, counter):
 
 
 def main():
+    global KERNEL, NOTE
+    name = "scale_tick_kernel (fused merge/ops/send)"
+    if "--pview" in sys.argv:
+        sys.argv.remove("--pview")
+        KERNEL = "pview_tick_kernel<false"
+        name = "pview_tick_kernel (partial-view union/fold/evict)"
+        NOTE = ("FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
+                "loads: uncalibrated for that width, MI355X_MICROARCH.md HBM section)")
     fetch, n1 = per_launch(sys.argv[1], "FETCH_SIZE")
     write, n2 = per_launch(sys.argv[2], "WRITE_SIZE")
     out = {
-        "kernel": "scale_tick_kernel (fused merge/ops/send)",
+        "kernel": name,
         "launches": min(n1, n2),
         "fetch_size_kib_raw": fetch,
         "write_size_kib": write,
         "read_bytes_per_launch": fetch * 1024 * 2,
         "write_bytes_per_launch": write * 1024,
         "bytes_per_launch": fetch * 1024 * 2 + write * 1024,
-        "correction": "FETCH_SIZE x2 (gfx950 counts half of 16-B/lane streaming reads)",
+        "correction": NOTE,
     }
     s = json.dumps(out, indent=1)
     if len(sys.argv) > 3:
