@@ -154,7 +154,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "xgmi_bytes_per_tick": xgmi, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
-                     "kernel": "pview_tick_kernel",
+                     "kernel": "pview_tick_kernel", "valu": _pview_valu(nodes, world, kern_ms),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
     }
     if world == 1 and cpu_baseline_on:
@@ -172,6 +172,23 @@ def _pview_traffic(nodes, world):
         return json.load(open(prof)).get("bytes_per_launch")
     except Exception:
         return None
+
+
+def _pview_valu(nodes, world, kern_ms):
+    """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per launch from the
+    committed PMC pass (profiles/pmc_sq_pview.json, scripts/gpu_run.sh) against the issue
+    capacity of the launch -- 1,024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
+    (MI355X_MICROARCH.md) -- over the live mean kernel time; one GPU, config 5 only."""
+    prof = os.path.join(ROOT, "profiles", "pmc_sq_pview.json")
+    if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
+        return None
+    try:
+        insts = json.load(open(prof))["counters"]["SQ_INSTS_VALU"]["per_launch"]
+    except Exception:
+        return None
+    capacity = 1024 * 2.4e9 / 4.0 * kern_ms * 1e-3
+    return {"bound": "valu-issue", "insts_per_launch": insts, "issue_capacity": capacity,
+            "frac": insts / capacity, "clock_ghz": 2.4}
 
 
 def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
