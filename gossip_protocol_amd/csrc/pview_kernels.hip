@@ -68,6 +68,12 @@ __device__ inline uint32_t pv_merge(uint32_t e, uint32_t v, uint32_t t5, uint32_
     const uint32_t add = (v != 0u && ((t5 - v) & 31u) < tr) ? v : 0u;
     return e ? upd : add;
 }
+// eviction order bin of a surviving entry: age * 32 + min(h0 + t - age - hb, 31), th0 = h0 + t
+__device__ inline uint32_t pv_bin(uint32_t v, uint32_t t5, uint32_t th0) {
+    const uint32_t age = (t5 - v) & 31u;
+    const int32_t e = int32_t(th0 - age) - int32_t(v >> 5);
+    return (age << 5) | uint32_t(e < 0 ? 0 : e > 31 ? 31 : e);
+}
 // the sender entry of a GOSSIP: hb + 1 and ts = t, or (1, t) when absent (MP1Node.cpp:237-243)
 __device__ inline uint32_t pv_event(uint32_t v, uint32_t t5) { return (((v >> 5) + 1u) << 5) | t5; }
 
@@ -149,15 +155,15 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
 
 // LDS of one row (20 KB: 8 rows per CU).  keys[cur] (the sorted union C) is dead once the
 // fold is done and then holds: the kept ids W [0, 256), the kept values (u16) at word 512,
-// the boundary-age hb histogram (2048 u16 bins) at words [1024, 2048).  keys[cur ^ 1] (the
-// last merge level's source) is dead after the tree and holds the age histogram (words
-// [0, 32)), the block-scan buffers (words [2040, 2048)) and, when no eviction is needed,
-// the survivor ids U (words [0, 256)).
+// the exact hb histogram of an e >= 31 boundary bin (2048 u16 bins) at words [1024, 2048).
+// keys[cur ^ 1] (the last merge level's source) is dead after the tree and holds the (age,
+// hb) eviction bins (1024 u16 counters, words [512, 1024)), the block-scan buffers (words
+// [2040, 2048)) and, when no eviction is needed, the survivor ids U (words [0, 256)).
 struct alignas(16) PvShared {
     uint32_t keys[2][kMaxKeys];          // merge ping-pong; then the regions above
     uint16_t vals[kMaxKeys];             // values by (source, slot); then survivor values
 };
-constexpr int kWValWord = 512, kHistWord = 1024;
+constexpr int kWValWord = 512, kHistWord = 1024, kBinWord = 512;
 
 __device__ inline int32_t lds_word(const PvShared &sh, const uint32_t *p) {
     return int32_t(p - &sh.keys[0][0]);
@@ -209,6 +215,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     const int32_t tid = threadIdx.x;
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
+    const uint32_t th0 = t + uint32_t(a.h0);
     const int32_t Pe = (k + 1) * kSlots;                // keys that can be real
     const uint64_t S_join = pv_seed(1, t, uint32_t(r)), S_remove = pv_seed(2, t, uint32_t(r)),
                    S_evict = pv_seed(3, t, uint32_t(r));
@@ -285,9 +292,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     }
     const int32_t beg = tid * Q;                               // the fold's Q keys per lane
     const uint32_t *C = sh.keys[cur];
-    uint32_t *const age_hist = sh.keys[cur ^ 1];              // dead after the tree
+    // keys[cur ^ 1] (the last level's source) is dead after the tree: it holds the eviction
+    // histogram over (age, hb) bins (1024 u16 counters at words [512, 1024)) and the scan
+    // buffers (words [2040, 2048))
+    uint32_t *const bins = sh.keys[cur ^ 1] + kBinWord;
     uint32_t *const scan_buf = sh.keys[cur ^ 1] + 2040;
-    if (tid < 32) age_hist[tid] = 0;
+    reinterpret_cast<uint2 *>(bins)[tid] = make_uint2(0u, 0u);
 
     pm.mark(2);
     // ---- 4. fold every id run that starts in this lane, in registers ------------------------
@@ -417,7 +427,6 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     uint32_t total = 0;
     const uint32_t base = block_scan(nloc, &total, scan_buf);
     const bool evict = int32_t(total) > V;
-    uint32_t *hist = sh.keys[cur] + kHistWord;                // 2048 hb bins, u16 pairs; C is dead
     if (!evict) {                                              // the survivors are the view
         uint32_t *Uid = sh.keys[cur ^ 1];
         uint16_t *Uval = sh.vals;                              // the gathered values are dead
@@ -431,37 +440,65 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         ro.vals_off = lds_half(sh, Uval);
         ro.len = int32_t(total);
     } else {
-        for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
-        for_each([&](uint32_t v, uint32_t) { atomicAdd(&age_hist[(t5 - v) & 31u], 1u); });
+        for_each([&](uint32_t v, uint32_t) {
+            const uint32_t b = pv_bin(v, t5, th0);
+            atomicAdd(&bins[b >> 1], 1u << ((b & 1u) * 16u));
+        });
     }
 
     pm.mark(4);
     // ---- 5b. eviction to V by (age, -hb, id) ------------------------------------------------
+    // Order key (age, -hb) as one bin index age * 32 + e, e = h0 + t - age - hb: every entry
+    // satisfies hb <= h0 + ts (a heartbeat grows by at most one per tick from h0, and every
+    // rule that sets ts = t sets hb <= h0 + t), so e >= 0, and within an age e ascends as hb
+    // descends.  Kept: every bin below the boundary bin, then boundary-bin entries in id
+    // order.  A boundary bin e < 31 holds one (age, hb); the last bin of an age (e >= 31)
+    // can hold several hb values -- then the exact boundary hb comes from an hb histogram.
     if (evict) {
-        __syncthreads();                                   // age histogram complete, hist zeroed
-        // boundary age astar: first cumulative count >= V (every wave computes it)
+        __syncthreads();                                   // bin histogram complete
         const int32_t lane = tid & 63;
-        uint32_t astar, need, at;
-        {
-            const uint32_t hv = lane < 32 ? age_hist[lane] : 0u;
-            uint32_t incl = hv;
+        uint32_t bstar, need, at;
+        {   // every wave: lane l sums bins [16 l, 16 l + 16), the lane holding the V-th entry
+            // walks its bins
+            const uint16_t *b16 = reinterpret_cast<const uint16_t *>(bins);
+            const uint4 *bw = reinterpret_cast<const uint4 *>(bins + 8 * lane);
+            uint32_t loc = 0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint4 x = bw[q];
+                loc += (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
+                       (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
+            }
+            uint32_t incl = loc;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t u = __shfl_up(incl, d, 64);
                 if (lane >= d) incl += u;
             }
-            const unsigned long long hit = __ballot(lane < 32 && incl >= uint32_t(V));
-            const int32_t ab = __builtin_ffsll(hit) - 1;
-            astar = uint32_t(ab);
-            need = uint32_t(V) - __shfl(incl - hv, ab, 64);    // kept at the boundary age
-            at = __shfl(hv, ab, 64);
+            const int32_t lb = __builtin_ffsll(__ballot(incl >= uint32_t(V))) - 1;
+            const uint32_t before = __shfl(incl - loc, lb, 64);
+            const uint32_t c = lane < 16 ? uint32_t(b16[16 * lb + lane]) : 0u;
+            uint32_t ci = c;
+#pragma unroll
+            for (int d = 1; d < 16; d <<= 1) {
+                const uint32_t u = __shfl_up(ci, d, 64);
+                if (lane >= d) ci += u;
+            }
+            const int32_t lh = __builtin_ffsll(__ballot(lane < 16 && before + ci >= uint32_t(V))) - 1;
+            bstar = uint32_t(16 * lb + lh);
+            at = __shfl(c, lh, 64);
+            need = uint32_t(V) - (before + __shfl(ci, lh, 64) - at);   // kept from the bin
         }
         pm.mark(7);
         const bool tie = at > need;
-        uint32_t hstar = 0, need2 = 0;
-        if (tie) {                                         // boundary hb among age == astar
+        const uint32_t astar = bstar >> 5;
+        uint32_t hstar = th0 - astar - (bstar & 31u), need2 = need;
+        if (tie && (bstar & 31u) == 31u) {                               // block-uniform: exact hb boundary
+            uint32_t *hist = sh.keys[cur] + kHistWord;     // 2048 hb bins, u16 pairs; C is dead
+            for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
+            __syncthreads();
             for_each([&](uint32_t v, uint32_t) {
-                if (((t5 - v) & 31u) == astar)
+                if (pv_bin(v, t5, th0) == bstar)
                     atomicAdd(&hist[(v >> 5) >> 1], 1u << (((v >> 5) & 1u) * 16u));
             });
             __syncthreads();
@@ -501,11 +538,13 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         pm.mark(8);
         // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
         uint32_t nt = 0, nk = 0;
+        // ties: the boundary bin's entries with hb == hstar (all of them unless e >= 31);
+        // plain keeps: lower bins, and boundary-bin entries with a larger hb or without a tie
         for_each([&](uint32_t v, uint32_t) {
-            const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
-            const bool is_tie = tie && age == astar && hb == hstar;
+            const uint32_t b = pv_bin(v, t5, th0), hb = v >> 5;
+            const bool is_tie = tie && b == bstar && hb == hstar;
             nt += is_tie ? 1u : 0u;
-            nk += (!is_tie && (age < astar || (age == astar && (!tie || hb > hstar)))) ? 1u : 0u;
+            nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
         });
         uint32_t sums = 0;
         const uint32_t ex = block_scan(nt | (nk << 16), &sums, scan_buf + 4);
@@ -515,9 +554,9 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
         for_each([&](uint32_t v, uint32_t x) {
-            const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
-            bool keep = age < astar || (age == astar && (!tie || hb > hstar));
-            if (tie && age == astar && hb == hstar) keep = tie_before++ < need2;
+            const uint32_t b = pv_bin(v, t5, th0), hb = v >> 5;
+            bool keep = b < bstar || (b == bstar && (!tie || hb > hstar));
+            if (tie && b == bstar && hb == hstar) keep = tie_before++ < need2;
             if (keep) {
                 Wid[w] = x;
                 Wval[w] = uint16_t(v);

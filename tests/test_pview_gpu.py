@@ -44,9 +44,23 @@ def eng_tick(eng):
 
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d_k%d" % c[:4])
 def test_pview_matches_oracle(case):
+    _run_case(case)
+
+
+# h0 = 100: an adopted orphan (hb 1, ts t) and its copies sit e = h0 + ts - hb >= 31 deep in
+# their age's eviction bins, so the boundary often falls in an age's last bin and takes the
+# exact hb-histogram path of the kernel; the long case reaches large e with h0 = 1
+@pytest.mark.parametrize("case", [(2000, 64, 3, 7, 10, 1, 8, 30000, 4, 30, 100),
+                                  (1000, 48, 4, 7, 5, 0, 10, 0, 6, 70, 1)],
+                         ids=["h0_100", "h0_1_70ticks"])
+def test_pview_eviction_bins_match_oracle(case):
+    _run_case(case[:-1], h0=case[-1])
+
+
+def _run_case(case, h0=1):
     n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
     kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
-              fail_ppm=ppm, seed=seed)
+              fail_ppm=ppm, seed=seed, h0=h0)
     orc = PviewOracle(n, **kw)
     rng = np.random.default_rng(seed)
     with PviewEngine(n, max_ticks=ticks, **kw) as eng:
