@@ -597,9 +597,12 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
         if (tid == 0) a.len_cur[lr] = len;
         return;
     }
-    const uint64_t jr = wave_sum32(ro.joins) | (uint64_t(wave_sum32(ro.removes)) << 16);
-    const uint64_t ev = wave_sum32(ro.evicts);
-    uint64_t mg = wave_sum32(ro.merged);
+    // per-lane counts are <= 15, so two 16-bit fields per word cannot carry in a wave sum
+    const uint32_t jrs = wave_sum32(ro.joins | (ro.removes << 16));
+    const uint32_t evm = wave_sum32(ro.evicts | (ro.merged << 16));
+    const uint64_t jr = jrs;                          // joins | removes << 16
+    const uint64_t ev = evm & 0xFFFFu;
+    uint64_t mg = evm >> 16;
     const uint64_t h = wave_sum64(ro.hsum);
     if (lane == 0) {
         uint64_t w0 = mg, w1 = jr | (ev << 32);
