@@ -176,9 +176,10 @@ def _pview_traffic(nodes, world):
 
 def _pview_valu(nodes, world, kern_ms):
     """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per launch from the
-    committed PMC pass (profiles/pmc_sq_pview.json, scripts/gpu_run.sh) against the issue
-    capacity of the launch -- 1,024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU instruction
-    (MI355X_MICROARCH.md) -- over the live mean kernel time; one GPU, config 5 only."""
+    committed PMC pass (profiles/pmc_sq_pview.json, scripts/gpu_run.sh) over the live mean
+    kernel time: wave64 VALU instructions issued per SIMD cycle (1,024 SIMDs at 2.4 GHz), and
+    that rate against the 4-cycle wave64 issue model (MI355X_MICROARCH.md, 'vector-instruction
+    ISSUE cost'); one GPU, config 5 only."""
     prof = os.path.join(ROOT, "profiles", "pmc_sq_pview.json")
     if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
         return None
@@ -186,9 +187,9 @@ def _pview_valu(nodes, world, kern_ms):
         insts = json.load(open(prof))["counters"]["SQ_INSTS_VALU"]["per_launch"]
     except Exception:
         return None
-    capacity = 1024 * 2.4e9 / 4.0 * kern_ms * 1e-3
-    return {"bound": "valu-issue", "insts_per_launch": insts, "issue_capacity": capacity,
-            "frac": insts / capacity, "clock_ghz": 2.4}
+    per_cycle = insts / (1024 * 2.4e9 * kern_ms * 1e-3)
+    return {"bound": "valu-issue", "insts_per_launch": insts, "insts_per_simd_cycle": per_cycle,
+            "frac_of_4cycle_issue": per_cycle * 4.0, "clock_ghz": 2.4}
 
 
 def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
