@@ -403,24 +403,25 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             if ((adopt >> jj) & 1u) { o_x = ssrc[jj]; o_p = ains[jj]; }
     }
     const bool multi = __ballot(n_orph > 1) != 0ull;          // wave-uniform
-    auto for_each = [&](auto &&f) {
+    // rb[e]: the eviction bin of res[e] (filled on the eviction path, computed once per slot)
+    uint32_t rb[Q];
+#pragma unroll
+    for (int e = 0; e < Q; ++e) rb[e] = 0;
+    const uint32_t fresh_bin = pv_bin(fresh, t5, th0);
+    auto for_each = [&](auto &&f) {                            // f(value, id, bin)
         if (!multi) {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
-                if (o_p == e) f(fresh, o_x);
-                if (e < Q && res[e]) f(res[e], rid[e]);
+                if (o_p == e) f(fresh, o_x, fresh_bin);
+                if (e < Q && res[e]) f(res[e], rid[e], rb[e]);
             }
         } else {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
-#ifdef GSP_PV_MULTI_LOOP
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
                 for (int jj = 0; jj < kJ; ++jj)
-                    if (((adopt >> jj) & 1u) && ains[jj] == e) f(fresh, ssrc[jj]);
-                if (e < Q && res[e]) f(res[e], rid[e]);
+                    if (((adopt >> jj) & 1u) && ains[jj] == e) f(fresh, ssrc[jj], fresh_bin);
+                if (e < Q && res[e]) f(res[e], rid[e], rb[e]);
             }
         }
     };
@@ -431,7 +432,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t *Uid = sh.keys[cur ^ 1];
         uint16_t *Uval = sh.vals;                              // the gathered values are dead
         uint32_t w = base;
-        for_each([&](uint32_t v, uint32_t x) {
+        for_each([&](uint32_t v, uint32_t x, uint32_t) {
             Uid[w] = x;
             Uval[w] = uint16_t(v);
             w++;
@@ -440,8 +441,9 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         ro.vals_off = lds_half(sh, Uval);
         ro.len = int32_t(total);
     } else {
-        for_each([&](uint32_t v, uint32_t) {
-            const uint32_t b = pv_bin(v, t5, th0);
+#pragma unroll
+        for (int e = 0; e < Q; ++e) rb[e] = pv_bin(res[e], t5, th0);
+        for_each([&](uint32_t, uint32_t, uint32_t b) {
             atomicAdd(&bins[b >> 1], 1u << ((b & 1u) * 16u));
         });
     }
@@ -497,8 +499,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             uint32_t *hist = sh.keys[cur] + kHistWord;     // 2048 hb bins, u16 pairs; C is dead
             for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
             __syncthreads();
-            for_each([&](uint32_t v, uint32_t) {
-                if (pv_bin(v, t5, th0) == bstar)
+            for_each([&](uint32_t v, uint32_t, uint32_t b) {
+                if (b == bstar)
                     atomicAdd(&hist[(v >> 5) >> 1], 1u << (((v >> 5) & 1u) * 16u));
             });
             __syncthreads();
@@ -540,8 +542,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t nt = 0, nk = 0;
         // ties: the boundary bin's entries with hb == hstar (all of them unless e >= 31);
         // plain keeps: lower bins, and boundary-bin entries with a larger hb or without a tie
-        for_each([&](uint32_t v, uint32_t) {
-            const uint32_t b = pv_bin(v, t5, th0), hb = v >> 5;
+        for_each([&](uint32_t v, uint32_t, uint32_t b) {
+            const uint32_t hb = v >> 5;
             const bool is_tie = tie && b == bstar && hb == hstar;
             nt += is_tie ? 1u : 0u;
             nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
@@ -553,8 +555,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
-        for_each([&](uint32_t v, uint32_t x) {
-            const uint32_t b = pv_bin(v, t5, th0), hb = v >> 5;
+        for_each([&](uint32_t v, uint32_t x, uint32_t b) {
+            const uint32_t hb = v >> 5;
             bool keep = b < bstar || (b == bstar && (!tie || hb > hstar));
             if (tie && b == bstar && hb == hstar) keep = tie_before++ < need2;
             if (keep) {
