@@ -295,7 +295,9 @@ typedef struct {
 
 typedef struct {
     int64_t tick, node_rounds, merges, sent, dropped, delivered, overflow, joins, removes, evicts;
-    uint64_t event_hash;   /* sum of mix64(kind, t, r, x); kinds 1 join, 2 remove, 3 evict */
+    uint64_t event_hash;   /* sum of h(kind, t, r, x) = mix64(kind, t, r, 0) + a 3-multiply
+                              finaliser of x (oracle: gsp_pv_event_mix); kinds 1 join,
+                              2 remove, 3 evict */
 } gsp_pview_digest;
 
 int gsp_pview_create(const gsp_pview_params *p, int device, gsp_pview **out);
