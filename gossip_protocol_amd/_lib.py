@@ -48,7 +48,7 @@ class GspScaleParams(ctypes.Structure):
     _fields_ = [("n", c_int32), ("fanout", c_int32), ("drop_pct", c_int32),
                 ("tremove", c_int32), ("h0", c_int32), ("fail_mode", c_int32),
                 ("fail_tick", c_int32), ("fail_ppm", c_int32), ("seed", c_uint64),
-                ("max_ticks", c_int32), ("tfail", c_int32)]
+                ("max_ticks", c_int32), ("tfail", c_int32), ("swim", c_int32)]
 
 
 class GspScaleDigest(ctypes.Structure):

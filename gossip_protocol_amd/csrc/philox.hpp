@@ -15,6 +15,7 @@ enum : uint32_t {
     kDomainSend = 0x53454E44u,  // "SEND": drop draw of one message
     kDomainFail = 0x4641494Cu,  // "FAIL": failure injection
     kDomainPeer = 0x50454552u,  // "PEER": scale-mode peer choice
+    kDomainPing = 0x50494E47u,  // "PING": SWIM probe target and probe paths
 };
 
 __host__ __device__ inline uint32_t philox_word0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,

@@ -34,13 +34,13 @@ struct Shard {
     gsp::RowxBufs x;               // row layout exchange buffers
     gsp::DevBuf<uint16_t> table[2];
     gsp::DevBuf<int32_t> own_hb, fail_tick, cnt_total[2], cnt_slice, cnt_all, out_dst, picks,
-        deg, off, fill, csr_src, err, tile_sum;
+        ping, deg, off, fill, csr_src, err, tile_sum;
     gsp::DevBuf<uint8_t> bitmap;
     gsp::DevBuf<unsigned long long> dig;
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
-        for (auto *x : {&own_hb, &fail_tick, &cnt_slice, &cnt_all, &out_dst, &picks, &deg, &off,
+        for (auto *x : {&own_hb, &fail_tick, &cnt_slice, &cnt_all, &out_dst, &picks, &ping, &deg, &off,
                         &fill, &csr_src, &err, &tile_sum})
             x->release();
         bitmap.release();
@@ -105,6 +105,7 @@ struct gsp_scale {
         a.nt_src = (policy >> 1) & 1;
         a.pipe = (policy >> 2) & 1;
         a.tfail = p.tfail;
+        a.swim = p.swim;
         a.count_rounds = rowmode || sh.g == 0;
         a.seed = p.seed;
         a.fail_tick = sh.fail_tick.p;
@@ -116,6 +117,7 @@ struct gsp_scale {
         a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
         a.out_dst = sh.out_dst.p;
         a.deg = sh.deg.p;
+        a.ping = sh.ping.p;
         a.bitmap = sh.bitmap.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
@@ -176,6 +178,8 @@ int validate_scale_params(const gsp_scale_params *p) {
     GSP_REQUIRE(p->fail_mode >= 0 && p->fail_mode <= 2, GSP_ERR_INVALID, "fail_mode=%d", p->fail_mode);
     GSP_REQUIRE(p->tfail == 0 || (p->tfail >= 1 && p->tfail < p->tremove), GSP_ERR_INVALID,
                 "tfail=%d: 0 (off) or 1..tremove-1", p->tfail);
+    GSP_REQUIRE(p->swim >= 0 && p->swim <= 8, GSP_ERR_INVALID, "swim=%d: 0 (off) or 1..8 paths",
+                p->swim);
     GSP_REQUIRE(p->max_ticks >= 1 && int64_t(p->h0) + p->max_ticks <= 2047, GSP_ERR_RANGE,
                 "h0 + max_ticks = %d exceeds the 11-bit packed heartbeat (2047)",
                 p->h0 + p->max_ticks);
@@ -199,6 +203,10 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     GSP_HIP(sh.own_hb.alloc(rows));
     GSP_HIP(sh.fail_tick.alloc(size_t(n)));
     GSP_HIP(sh.out_dst.alloc(rows * s->p.fanout));
+    if (s->p.swim > 0) {
+        GSP_HIP(sh.ping.alloc(rows));
+        GSP_HIP(hipMemsetAsync(sh.ping.p, 0xFF, rows * 4, st));   // -1: no probe yet
+    }
     GSP_HIP(sh.deg.alloc(size_t(n)));
     GSP_HIP(sh.off.alloc(rows + 1));
     GSP_HIP(sh.fill.alloc(rows));
@@ -360,6 +368,9 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     const bool sharded = shards > 1 || nccl_id != nullptr;
     s->sliced = sharded && layout == GSP_SHARD_COLUMNS;
     s->rowmode = sharded && layout == GSP_SHARD_ROWS;
+    // column shards choose peers in scale_resolve_kernel, which has no probe target
+    GSP_REQUIRE(!(s->sliced && p->swim > 0), GSP_ERR_INVALID,
+                "gsp_scale: swim needs the fused or the row layout (column shards: %d)", shards);
     const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
     s->stride = s->width / (s->sliced ? shards : 1);

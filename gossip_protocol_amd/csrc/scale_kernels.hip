@@ -195,7 +195,11 @@ __device__ inline int32_t next_distinct_rank(uint32_t u, int32_t cnt, int32_t k,
 // kTfail: TFAIL suspicion (a.tfail > 0): a sender's payload holds only the members it could
 // gossip at send time (t - 1 - ts < tfail), and only members with t - ts < tfail get a
 // presence bit (peer choice) and count.
-template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe = false, bool kTfail = false>
+// kSwim: SWIM ping/ack probing (a.swim paths, oracle/scale_oracle.c): the probe this row sent at
+// t - 1 is resolved after the merges (answered: ts of the target = t; unanswered: ts = t -
+// TREMOVE, so the TREMOVE scan removes it), and wave 0 picks this tick's probe target.
+template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe = false, bool kTfail = false,
+          bool kSwim = false>
 __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
     constexpr bool kNtOwn = (kPolicy & 1) != 0, kNtSrc = (kPolicy & 2) != 0;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // fused: stride/32 words
@@ -260,6 +264,23 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         const uint32_t age = (t32m1 - (w & pc.low5)) & pc.low5;
         return w & pk_sub(pc.zero, pk_min(pk_subc(tfx2, age), pc.one));
     };
+    // kSwim: the probe of t - 1 (target pcol, read before wave 0 rewrites a.ping[lr] below the
+    // block reduction's barrier); one direct + a.swim - 1 indirect paths, each with a drop draw
+    int32_t pcol = -1;
+    uint32_t pts = 0;                  // the target's new ts mod 32
+    if (kSwim && !kInit) {
+        pcol = a.ping[lr];
+        if (pcol >= 0) {
+            bool ok = false;
+            for (int32_t i = 0; i < a.swim; ++i) {
+                const uint32_t dr = draw_u31(kDomainPing, a.seed, uint32_t(t - 1), uint32_t(r),
+                                             uint32_t(pcol), uint32_t(i));
+                ok = ok || int32_t(dr % 100u) >= a.drop_pct;
+            }
+            ok = ok && t <= a.fail_tick[pcol];
+            pts = ok ? t5 : ((t5 - tr) & 31u);
+        }
+    }
     const int64_t stride = a.stride;
     const uint16_t *own_prev = a.prev + int64_t(lr) * stride;
     uint16_t *own_cur = a.cur + int64_t(lr) * stride;
@@ -359,6 +380,11 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             }
             const int64_t dr = int64_t(r) - gc0;      // never list yourself (MP1Node.cpp:290)
             if (dr >= 0 && dr < kEntriesPerLane) patch16(e, int(dr), [](uint32_t) { return 0u; });
+            if (kSwim && pcol >= 0) {                 // the probe's answer (or its absence)
+                const int64_t dp = int64_t(pcol) - gc0;
+                if (dp >= 0 && dp < kEntriesPerLane)
+                    patch16(e, int(dp), [pts](uint32_t old) { return old ? ((old & 0xFFE0u) | pts) : 0u; });
+            }
             ws[0] = e.x; ws[1] = e.y; ws[2] = e.z; ws[3] = e.w;
         }
 
@@ -469,6 +495,15 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         if (lane == 0 && sent) {
             atomicAdd(&dig[kDigSent], sent);
             atomicAdd(&dig[kDigDropped], dropped);
+        }
+        if (kSwim) {                                  // this tick's probe target
+            int32_t p = -1;
+            if (cnt > 0) {
+                const uint32_t u = draw_u31(kDomainPing, a.seed, uint32_t(t), uint32_t(r), 0u, 0x100u);
+                p = wave_select([&](int32_t w) { return s_bits[w]; }, per, lane_cnt, pre,
+                                u % uint32_t(cnt), lane);
+            }
+            if (lane == 0) a.ping[lr] = p;
         }
     }
 }
@@ -647,6 +682,9 @@ hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st)
     const size_t lds = scale_lds_bytes(a.stride, slice);
     if (slice)
         hipLaunchKernelGGL((scale_tick_kernel<true, true, 1, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a);
+    else if (a.swim > 0)
+        hipLaunchKernelGGL((scale_tick_kernel<true, false, 1, 0, false, false, true>), dim3(a.rows),
+                           dim3(kScaleBlock), lds, st, a);
     else
         hipLaunchKernelGGL((scale_tick_kernel<true, false, 1, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a);
     return hipGetLastError();
@@ -655,6 +693,15 @@ hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st)
 template <bool kSlice, int kMerge>
 void launch_tick_policy(const ScaleTickArgs &a, int policy, size_t lds, hipStream_t st) {
     const dim3 grid(a.rows), block(kScaleBlock);
+    if constexpr (!kSlice) {
+        if (a.swim > 0) {
+            if (a.tfail > 0)
+                hipLaunchKernelGGL((scale_tick_kernel<false, false, kMerge, 1, false, true, true>), grid, block, lds, st, a);
+            else
+                hipLaunchKernelGGL((scale_tick_kernel<false, false, kMerge, 1, false, false, true>), grid, block, lds, st, a);
+            return;
+        }
+    }
     if (a.tfail > 0) {
         hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, false, true>), grid, block, lds, st, a);
         return;

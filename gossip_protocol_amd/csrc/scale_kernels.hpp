@@ -7,6 +7,7 @@
 //                           all n rows, columns [col0, col0 + stride), stride = width / G.
 //   own_hb[rows], fail_tick[n], cnt[2][n] (member count by tick parity)
 //   out_dst[rows * fanout]  this tick's messages (dst id or -1) of each sender slot
+//   ping[rows]              swim: this tick's probe target (global id or -1)
 //   deg[n], off[n + 1], fill[n], csr_src[n * fanout] (+ csr_slot)  next tick's receiver CSR
 //   dig[ticks][kDigSlots][kDigFields]   sharded per-tick digest accumulators
 // ts is kept modulo 32: every timestamp the protocol ever compares is within 20 ticks of
@@ -43,6 +44,7 @@ struct ScaleTickArgs {
     int32_t pipe;                // software-pipelined chunk loads (packed merge, policy 1)
     int32_t tfail;               // TFAIL suspicion: 0 off, else members this stale are not
                                  // gossiped / chosen / counted
+    int32_t swim;                // SWIM probing: 0 off, else 1 direct + swim - 1 indirect paths
     int32_t count_rounds;        // this shard adds node-rounds / merges / sends to the digest
     uint64_t seed;
     const int32_t *fail_tick;    // [n] global
@@ -54,6 +56,7 @@ struct ScaleTickArgs {
     const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
     int32_t *out_dst;            // [rows * fanout]
     int32_t *deg;                // [n] messages per destination (atomic)
+    int32_t *ping;               // swim: [rows] probe target of the last send (-1 none)
     uint8_t *bitmap;             // slice mode: [rows][stride / 8] presence bits
     unsigned long long *dig;     // [kDigSlots][kDigFields] of this tick
     int32_t *err;                // [1] capacity error flag

@@ -35,15 +35,17 @@ class ScaleEngine:
     between shards).  Default: one GPU, full rows, fused tick kernel.
     tfail > 0: TFAIL suspicion (members tfail or more ticks stale are listed but not gossiped,
     chosen or counted); 0 is the reference's protocol.
+    swim = s > 0: SWIM ping/ack probing, one probe target per node per tick over 1 direct + s - 1
+    indirect paths (answered: ts refreshed; unanswered: removed); fused or row layout only.
     """
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
                  fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0, group=1,
-                 rank=0, world=1, nccl_id=None, layout="columns", tfail=0):
+                 rank=0, world=1, nccl_id=None, layout="columns", tfail=0, swim=0):
         self.params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
                                           h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
                                           fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks,
-                                          tfail=tfail)
+                                          tfail=tfail, swim=swim)
         self._h = ctypes.c_void_p()
         lay = LAYOUTS[layout]
         if nccl_id is not None:

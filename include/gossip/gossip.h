@@ -197,6 +197,11 @@ typedef struct {
                            1..tremove-1: a member whose heartbeat is tfail or more ticks
                            old is suspected -- listed until TREMOVE but not gossiped, not
                            chosen as a peer and not counted (DESIGN.md "Scale mode")   */
+    int32_t swim;       /* SWIM ping/ack probing (spec p.3, not in the reference): 0 off;
+                           s = 1..8: each node probes one member per tick over 1 direct +
+                           s - 1 indirect paths; answered -> ts refreshed, unanswered ->
+                           removed at the next tick (DESIGN.md "Scale mode").  Fused or
+                           row layout only                                             */
 } gsp_scale_params;
 
 typedef struct {

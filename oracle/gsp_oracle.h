@@ -49,6 +49,8 @@ typedef struct {
     int32_t tfail;      /* 0: off (the reference: TFAIL unused); else members with
                            t - ts >= tfail are suspected: not gossiped, not chosen as
                            peers, not counted (MP1Node.h:22, spec p.3)         */
+    int32_t swim;       /* 0: off; s >= 1: SWIM ping/ack probing with one direct path
+                           and s - 1 indirect (ping-req) paths (spec p.3)      */
 } gsp_scale_cfg;
 
 typedef struct {

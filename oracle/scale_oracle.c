@@ -19,6 +19,17 @@
  * peer choice and of its member count.  The GPU engine stores entries packed
  * (hb:11 | ts mod 32:5); this restatement keeps absolute values so that parity tests
  * prove the packing loses nothing observable.
+ * SWIM ping/ack probing (mp1_specifications.pdf p.3 allows it, the reference
+ * does not implement it): with cfg.swim = s >= 1, every alive node r also picks ONE probe
+ * target p per tick -- Philox(PING; t, r, 0, 0x100) % cnt over the same member order as its
+ * gossip peers.  The probe (ping + ack, one round trip) is resolved in r's tick t + 1, after
+ * r's gossip merges and before its TREMOVE scan: it is answered iff p is alive at t + 1 and
+ * at least one of s paths survives its drop draw (Philox(PING; t, r, p, i) % 100 >=
+ * drop_pct, i = 0 direct, 1..s-1 indirect ping-req relays).  Answered: r refreshes p's
+ * timestamp (ts = t + 1, hb unchanged, so hb <= h0 + t still holds).  Unanswered: r declares
+ * p failed -- ts = (t + 1) - TREMOVE, so the scan of the same tick removes it (one remove
+ * event).  The probe target was listed when chosen and merges never remove, so it is listed
+ * at resolution time.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -33,6 +44,7 @@ struct gsp_scale_oracle {
     uint8_t *pres[2];
     int32_t *hb[2], *ts[2];
     int32_t *own_hb, *fail_tick, *cnt;
+    int32_t *ping;                  /* swim: probe target of each node's last send, or -1 */
     int32_t *msrc, *mdst;
     int64_t nmsg, mcap;
 };
@@ -111,11 +123,22 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
             o->mdst[o->nmsg] = dst;
             o->nmsg++;
         }
+        if (c->swim > 0) {      /* the probe target: one more rank-select over the same order */
+            o->ping[s] = -1;
+            if (cnt > 0) {
+                int32_t rk = (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)t,
+                                                      (uint32_t)s, 0, 0x100) % (uint32_t)cnt);
+                int32_t seen = -1;
+                for (int32_t x = 0; x < n; ++x)
+                    if (ps[x] && gossipable(c, t, tss[x]) && ++seen == rk) { o->ping[s] = x; break; }
+            }
+        }
     }
 }
 
 gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg) {
-    if (!cfg || cfg->n < 2 || cfg->fanout < 1 || cfg->fanout > 60) return NULL;
+    if (!cfg || cfg->n < 2 || cfg->fanout < 1 || cfg->fanout > 60 ||
+        cfg->swim < 0 || cfg->swim > 8) return NULL;
     gsp_scale_oracle *o = calloc(1, sizeof *o);
     o->c = *cfg;
     const int32_t n = cfg->n;
@@ -128,6 +151,8 @@ gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg) {
     o->own_hb = calloc(n, sizeof(int32_t));
     o->fail_tick = calloc(n, sizeof(int32_t));
     o->cnt = calloc(n, sizeof(int32_t));
+    o->ping = malloc(sizeof(int32_t) * n);
+    for (int32_t r = 0; r < n; ++r) o->ping[r] = -1;
     compute_fail_ticks(o);
     /* tick 0: pre-joined, every other node present with (h0, 0) */
     for (int32_t r = 0; r < n; ++r) {
@@ -149,6 +174,7 @@ void gsp_scale_oracle_destroy(gsp_scale_oracle *o) {
     if (!o) return;
     for (int b = 0; b < 2; ++b) { free(o->pres[b]); free(o->hb[b]); free(o->ts[b]); }
     free(o->own_hb); free(o->fail_tick); free(o->cnt); free(o->msrc); free(o->mdst);
+    free(o->ping);
     free(o);
 }
 
@@ -212,6 +238,14 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
                     d->joins++; d->event_hash += gsp_event_mix(1, t, r, x);
                 }
             }
+        }
+        if (c->swim > 0 && o->ping[r] >= 0) {   /* resolve the probe sent at t - 1 */
+            const int32_t p = o->ping[r];
+            int ok = 0;
+            for (int32_t i = 0; i < c->swim; ++i)
+                ok |= (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)(t - 1), (uint32_t)r,
+                                               (uint32_t)p, (uint32_t)i) % 100u) >= c->drop_pct;
+            if (P[p]) S[p] = (ok && alive_at(o, p, t)) ? t : t - T;
         }
         o->own_hb[r] += 1;
         int32_t live = 0;

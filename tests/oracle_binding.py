@@ -20,7 +20,7 @@ class ScaleCfg(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("fanout", ctypes.c_int32), ("drop_pct", ctypes.c_int32),
                 ("tremove", ctypes.c_int32), ("h0", ctypes.c_int32), ("fail_mode", ctypes.c_int32),
                 ("fail_tick", ctypes.c_int32), ("fail_ppm", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32), ("swim", ctypes.c_int32)]
 
 
 class TickDigest(ctypes.Structure):
@@ -124,10 +124,10 @@ class ScaleOracle:
     """The scale-protocol restatement (oracle/scale_oracle.c)."""
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=0, fail_tick=10,
-                 fail_ppm=0, seed=0x5EED, tfail=0):
+                 fail_ppm=0, seed=0x5EED, tfail=0, swim=0):
         self.L = load_oracle()
         self.cfg = ScaleCfg(n, fanout, drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm, seed,
-                            tfail)
+                            tfail, swim)
         self.h = self.L.gsp_scale_oracle_create(ctypes.byref(self.cfg))
         assert self.h, "oracle create failed"
         self.n = n

@@ -136,6 +136,55 @@ def test_tfail_matches_oracle(case, shards, layout, merge, tfail):
     plain.close()
 
 
+SWIM_CASES = [
+    # (case, shards, layout, merge, tfail, swim): SWIM ping/ack probing
+    (CASES[1], 1, "columns", 1, 0, 2),
+    (CASES[1], 1, "columns", 0, 0, 1),
+    (CASES[3], 1, "columns", 1, 0, 1),
+    (CASES[4], 1, "columns", 1, 0, 3),
+    (CASES[2], 1, "columns", 1, 5, 2),
+    (CASES[1], 3, "rows", 1, 0, 2),
+    (CASES[3], 2, "rows", 1, 5, 1),
+]
+
+
+@pytest.mark.parametrize("case,shards,layout,merge,tfail,swim", SWIM_CASES,
+                         ids=lambda x: "n%d_f%d_d%d_m%d" % x[:4] if isinstance(x, tuple) else str(x))
+def test_swim_matches_oracle(case, shards, layout, merge, tfail, swim):
+    """SWIM probing: one probe target per node per tick, answered -> ts refreshed, unanswered
+    -> removed at the next tick.  Digests every tick, messages and rows vs the oracle."""
+    n, f, drop, mode, ftick, ppm, seed, ticks = case
+    orc = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                      seed=seed, tfail=tfail, swim=swim)
+    plain = ScaleOracle(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+                        fail_ppm=ppm, seed=seed, tfail=tfail)
+    differs = False
+    with ScaleEngine(n, fanout=f, drop_pct=drop, fail_mode=mode, fail_tick=ftick, fail_ppm=ppm,
+                     seed=seed, max_ticks=ticks, group=shards, layout=layout, tfail=tfail,
+                     swim=swim) as eng:
+        eng.set_merge(merge)
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            differs |= want != plain.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d" % t
+            if t % 9 == 0 or t == ticks:
+                src, dst = orc.messages()
+                m = eng.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+                _compare_state(eng, orc, n, range(t % 5, n, 11))
+        _compare_state(eng, orc, n, range(0, n, 3))
+    assert differs, "probing changed nothing: the case does not exercise SWIM"
+    orc.close()
+    plain.close()
+
+
+def test_swim_rejects_column_shards():
+    with pytest.raises(Exception, match="swim"):
+        ScaleEngine(256, group=2, layout="columns", swim=1)
+
+
 def test_rccl_rank_path_one_rank():
     """The RCCL code path (ncclCommInitRank, all-gather, all-reduce MAX) with a world of one:
     a one-rank communicator still runs the column protocol and must match the oracle."""

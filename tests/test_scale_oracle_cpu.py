@@ -47,3 +47,58 @@ def test_tfail_invariants():
         assert np.all(t - ts[listed] < tr)
     o.close()
     plain.close()
+
+
+# ---- SWIM ping/ack probing (mp1_specifications.pdf p.3; not in the reference).
+# Build-defined like TFAIL: pinned by invariants here, GPU vs oracle in tests/test_scale_gpu.py.
+
+def test_swim_answered_probes_change_only_timestamps():
+    """No drops, no failures: every probe is answered, so nothing is removed and the digests
+    equal the plain protocol's; a probe target's ts is refreshed to the resolving tick."""
+    kw = dict(fanout=3, drop_pct=0, fail_mode=0, seed=5)
+    o, d = _run(80, 30, swim=2, **kw)
+    plain, pd = _run(80, 30, **kw)
+    assert d == pd
+    assert all(x["removes"] == 0 for x in d)
+    fresher = 0
+    for r in range(80):
+        pres, hb, ts = o.row(r)
+        pp, ph, pt = plain.row(r)
+        assert np.array_equal(pres, pp) and np.array_equal(hb, ph)
+        assert np.all(ts >= pt)                    # refreshes only move ts forward
+        fresher += int(np.sum(ts != pt))
+    assert fresher > 0
+    o.close()
+    plain.close()
+
+
+def test_swim_unanswered_probes_remove_their_target():
+    """drop_pct = 100: no path survives, so every alive node removes its probe target at the
+    next tick -- n removals per tick until TREMOVE."""
+    n, tr = 64, 20
+    o, d = _run(n, tr - 1, swim=3, fanout=3, drop_pct=100, fail_mode=0, seed=9, tremove=tr)
+    assert [x["removes"] for x in d] == [n] * (tr - 1)
+    for r in range(n):
+        assert int(o.row(r)[0].sum()) == n - 1 - (tr - 1)
+    o.close()
+
+
+def test_swim_detects_crashes_before_tremove():
+    """Crashed members are removed by probes before the TREMOVE timeout could remove them;
+    without probing the first removal comes TREMOVE ticks after the last heartbeat."""
+    kw = dict(fanout=3, drop_pct=0, fail_mode=1, fail_tick=5, fail_ppm=100000, seed=3)
+    o, d = _run(128, 20, swim=1, **kw)
+    plain, pd = _run(128, 20, **kw)
+    early = sum(x["removes"] for x in d[:15])
+    assert early > 0 and sum(x["removes"] for x in pd[:15]) == 0
+    dead = {r for r in range(128) if o.fail_tick(r) < 20}
+    for r in range(128):
+        if r in dead:
+            continue
+        pres = o.row(r)[0]
+        gone = [x for x in dead if not pres[x]]
+        live_gone = [x for x in range(128) if x not in dead and x != r and not pres[x]]
+        assert not live_gone                        # no drops: a live member is never removed
+        assert len(gone) <= len(dead)
+    o.close()
+    plain.close()
