@@ -81,15 +81,36 @@ __device__ inline uint32_t key_id(uint32_t k) { return k >> 11; }
 __device__ inline uint32_t key_src(uint32_t k) { return (k >> 8) & 7u; }
 __device__ inline uint32_t key_slot(uint32_t k) { return k & 255u; }
 
-__device__ inline uint32_t wave_sum32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+// Wave64 inclusive scan on the DPP network: four row_shr steps scan each 16-lane row, then
+// row_bcast:15 (into rows 1, 3) and row_bcast:31 (into rows 2, 3) carry the row totals -- six
+// v_add_u32_dpp, where __shfl_up costs a ds_bpermute round trip plus index and select work per
+// step.  Lanes a shift or a row mask leaves out add 0 (old = 0).
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp_take(uint32_t x) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), kCtrl, kRowMask, 0xF, false));
 }
-__device__ inline uint64_t wave_sum64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += dpp_take<0x111>(x);            // row_shr:1
+    x += dpp_take<0x112>(x);            // row_shr:2
+    x += dpp_take<0x114>(x);            // row_shr:4
+    x += dpp_take<0x118>(x);            // row_shr:8
+    x += dpp_take<0x142, 0xA>(x);       // row_bcast:15
+    x += dpp_take<0x143, 0xC>(x);       // row_bcast:31
+    return x;
+}
+// value of lane l (wave-uniform l, from a ballot): one v_readlane
+__device__ __forceinline__ uint32_t lane_of(uint32_t x, int32_t l) {
+    return uint32_t(__builtin_amdgcn_readlane(int(x), l));
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_readlane(int(wave_incl_scan(v)), 63));
+}
+// 64-bit wave sum (mod 2^64) from three 32-bit scans: the low word in two 16-bit halves (each
+// sum < 2^22, no carry lost) and the high word mod 2^32
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+    const uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);
+    const uint64_t a = wave_sum32(lo & 0xFFFFu), b = wave_sum32(lo >> 16), c = wave_sum32(hi);
+    return a + (b << 16) + (c << 32);
 }
 
 // exclusive block scan over the 256 lanes; *total = sum of all lanes.  One barrier: the
@@ -97,12 +118,7 @@ __device__ inline uint64_t wave_sum64(uint64_t v) {
 // scan's barrier has retired every read of it.
 __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_wave) {
     const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += u;
-    }
+    const uint32_t incl = wave_incl_scan(v);
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
     uint32_t before = 0, all = 0;
@@ -471,25 +487,15 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 loc += (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
                        (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
             }
-            uint32_t incl = loc;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t u = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += u;
-            }
+            const uint32_t incl = wave_incl_scan(loc);
             const int32_t lb = __builtin_ffsll(__ballot(incl >= uint32_t(V))) - 1;
-            const uint32_t before = __shfl(incl - loc, lb, 64);
+            const uint32_t before = lane_of(incl - loc, lb);
             const uint32_t c = lane < 16 ? uint32_t(b16[16 * lb + lane]) : 0u;
-            uint32_t ci = c;
-#pragma unroll
-            for (int d = 1; d < 16; d <<= 1) {
-                const uint32_t u = __shfl_up(ci, d, 64);
-                if (lane >= d) ci += u;
-            }
+            const uint32_t ci = wave_incl_scan(c);      // c = 0 beyond lane 15
             const int32_t lh = __builtin_ffsll(__ballot(lane < 16 && before + ci >= uint32_t(V))) - 1;
             bstar = uint32_t(16 * lb + lh);
-            at = __shfl(c, lh, 64);
-            need = uint32_t(V) - (before + __shfl(ci, lh, 64) - at);   // kept from the bin
+            at = lane_of(c, lh);
+            need = uint32_t(V) - (before + lane_of(ci, lh) - at);   // kept from the bin
         }
         pm.mark(7);
         const bool tie = at > need;
@@ -515,27 +521,17 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 loc += (x.x & 0xFFFFu) + (x.x >> 16) + (x.y & 0xFFFFu) + (x.y >> 16) +
                        (x.z & 0xFFFFu) + (x.z >> 16) + (x.w & 0xFFFFu) + (x.w >> 16);
             }
-            uint32_t incl = loc;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t u = __shfl_up(incl, d, 64);
-                if (lane >= d) incl += u;
-            }
+            const uint32_t incl = wave_incl_scan(loc);
             const unsigned long long hit = __ballot(incl >= need);
             const int32_t lb = __builtin_ffsll(hit) - 1;
             // lanes 0..31 take the boundary lane's 32 bins (descending hb) and scan them
-            const uint32_t before = __shfl(incl - loc, lb, 64);
+            const uint32_t before = lane_of(incl - loc, lb);
             const uint32_t c = lane < 32 ? uint32_t(h16[2047 - 32 * lb - lane]) : 0u;
-            uint32_t ci = c;
-#pragma unroll
-            for (int d = 1; d < 32; d <<= 1) {
-                const uint32_t u = __shfl_up(ci, d, 64);
-                if (lane >= d) ci += u;
-            }
+            const uint32_t ci = wave_incl_scan(c);      // c = 0 beyond lane 31
             const unsigned long long hit2 = __ballot(lane < 32 && before + ci >= need);
             const int32_t lh = __builtin_ffsll(hit2) - 1;
             hstar = uint32_t(2047 - 32 * lb - lh);
-            need2 = need - before - (__shfl(ci, lh, 64) - __shfl(c, lh, 64));  // kept among ties
+            need2 = need - before - (lane_of(ci, lh) - lane_of(c, lh));  // kept among ties
         }
         pm.mark(8);
         // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
