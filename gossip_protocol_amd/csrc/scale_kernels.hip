@@ -14,6 +14,7 @@
 // so the kernel is HBM-bound at (2 + k) * stride * 2 bytes per row with k messages.
 #include "philox.hpp"
 #include "scale_kernels.hpp"
+#include "wave_ops.hpp"
 
 namespace gsp {
 namespace {
@@ -135,11 +136,7 @@ __device__ inline void st16(uint16_t *p, const uint32_t (&w)[4]) {
     else *q = v;
 }
 
-__device__ inline uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
+__device__ inline uint64_t wave_sum_u64(uint64_t v) { return wave_sum64(v); }
 
 // rank-th set bit (0-based) of a bitmap of `words` 32-bit words, by one wave; -1 if none.
 // lane_cnt / pre: this lane's popcount over its words and the exclusive prefix.
@@ -163,17 +160,12 @@ __device__ inline int32_t wave_select(W word, int32_t per, uint32_t lane_cnt, ui
     }
     const unsigned long long owner = __ballot(mine);
     if (!owner) return -1;
-    return __shfl(col, __builtin_ffsll(owner) - 1, 64);
+    return int32_t(lane_of(uint32_t(col), __builtin_ffsll(owner) - 1));
 }
 
-__device__ inline uint32_t wave_excl_prefix(uint32_t v, int32_t lane, uint32_t *total) {
-    uint32_t incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += u;
-    }
-    *total = __shfl(incl, 63, 64);
+__device__ inline uint32_t wave_excl_prefix(uint32_t v, int32_t, uint32_t *total) {
+    const uint32_t incl = wave_incl_scan(v);
+    *total = lane_of(incl, 63);
     return incl - v;
 }
 
