@@ -94,3 +94,18 @@ def test_no_gpu_fails_loudly():
     assert L.gsp_create(ctypes.byref(p), 0, 0, 1, None, ctypes.byref(h)) != 0
     sp = _lib.GspScaleParams(n=1024, fanout=3, tremove=20, h0=1, max_ticks=16)
     assert L.gsp_scale_create(ctypes.byref(sp), 0, ctypes.byref(h)) != 0
+
+
+def test_scale_variant_params_validated_before_the_device():
+    """tfail / swim ranges are checked by the C ABI before any HIP call (GSP_ERR_INVALID = -1),
+    in-range values get past validation (and fail later, at the device, without a GPU)."""
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    base = dict(n=1024, fanout=3, tremove=20, h0=1, max_ticks=16)
+    for bad in (dict(swim=-1), dict(swim=9), dict(tfail=20), dict(tfail=-2)):
+        sp = _lib.GspScaleParams(**base, **bad)
+        assert L.gsp_scale_create(ctypes.byref(sp), 0, ctypes.byref(h)) == -1, bad
+    if L.gsp_device_count() == 0:
+        for ok in (dict(swim=8), dict(tfail=5, swim=1)):
+            sp = _lib.GspScaleParams(**base, **ok)
+            assert L.gsp_scale_create(ctypes.byref(sp), 0, ctypes.byref(h)) not in (0, -1), ok
