@@ -656,13 +656,14 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
             sslot[jj] = __builtin_amdgcn_readlane(my_slot, jj);
         }
         pm.mark(0);
-        // one variant per key count (own view + k sender views), k = 5 and 6, 7 sharing
+        // one variant per key count (own view + k sender views)
         if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 2) pv_merge_row<3>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else if (k == 4) pv_merge_row<5>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k <= 5) pv_merge_row<6>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k == 5) pv_merge_row<6>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
+        else if (k == 6) pv_merge_row<7>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         else pv_merge_row<8>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
         pm.mark(5);
     }
