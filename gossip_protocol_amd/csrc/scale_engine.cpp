@@ -140,6 +140,8 @@ struct gsp_scale {
         r.cnt_total = sh.cnt_total[t & 1].p;
         r.bitmap = sh.bitmap.p;
         r.picks = sh.picks.p;
+        r.swim = p.swim;
+        r.ping = sh.ping.p;
         r.out_dst = sh.out_dst.p;
         r.deg = sh.deg.p;
         r.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
@@ -216,7 +218,7 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     if (s->sliced) {
         GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
         GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards));
-        GSP_HIP(sh.picks.alloc(size_t(n) * s->p.fanout));
+        GSP_HIP(sh.picks.alloc(size_t(n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0))));
         GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8)));
     }
     if (s->rowmode)
@@ -249,7 +251,7 @@ int exchange_counts(gsp_scale *s) {
 
 // all-reduce MAX of the resolved picks (each pick is resolved by exactly one shard)
 int exchange_picks(gsp_scale *s) {
-    const size_t cnt = size_t(s->p.n) * s->p.fanout;
+    const size_t cnt = size_t(s->p.n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0));
     if (s->comm) {
         Shard &sh = s->local[0];
         GSP_NCCL(ncclAllReduce(sh.picks.p, sh.picks.p, cnt, ncclInt32, ncclMax, s->comm, s->st));
@@ -270,7 +272,7 @@ int resolve_sends(gsp_scale *s, int32_t t) {
     // 2 (G-1)/G of n*f*4 B
     const double G = double(s->shards), n = double(s->p.n);
     s->perf.xgmi_bytes += double(s->local.size()) * (G - 1.0) *
-                          (n * 4.0 + 2.0 * n * s->p.fanout * 4.0 / G);
+                          (n * 4.0 + 2.0 * n * (s->p.fanout + (s->p.swim > 0 ? 1 : 0)) * 4.0 / G);
     if (int rc = exchange_counts(s)) return rc;
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(sh, t), s->st));
     if (int rc = exchange_picks(s)) return rc;
@@ -368,9 +370,6 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     const bool sharded = shards > 1 || nccl_id != nullptr;
     s->sliced = sharded && layout == GSP_SHARD_COLUMNS;
     s->rowmode = sharded && layout == GSP_SHARD_ROWS;
-    // column shards choose peers in scale_resolve_kernel, which has no probe target
-    GSP_REQUIRE(!(s->sliced && p->swim > 0), GSP_ERR_INVALID,
-                "gsp_scale: swim needs the fused or the row layout (column shards: %d)", shards);
     const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
     s->stride = s->width / (s->sliced ? shards : 1);

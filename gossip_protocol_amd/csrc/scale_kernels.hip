@@ -508,8 +508,9 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
     const int32_t s = int32_t(blockIdx.x) * 4 + int32_t(threadIdx.x >> 6);
     if (s >= a.n) return;
     const int32_t F = a.fanout;
+    const int32_t W = F + (a.swim > 0 ? 1 : 0);        // pick slots per sender
     if (a.tick > a.fail_tick[s]) {
-        if (lane < F) a.picks[int64_t(s) * F + lane] = -1;
+        if (lane < W) a.picks[int64_t(s) * W + lane] = -1;
         return;
     }
     const uint32_t c = lane < a.shards ? uint32_t(a.cnt_all[int64_t(lane) * a.n + s]) : 0u;
@@ -545,7 +546,29 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
                 pick = int32_t(int64_t(a.shard) * a.stride + col);
             }
         }
-        if (lane == 0) a.picks[int64_t(s) * F + kk] = pick;
+        if (lane == 0) a.picks[int64_t(s) * W + kk] = pick;
+    }
+    if (a.swim > 0) {      // the probe target: one more rank-select over the same global order
+        int32_t pick = -1;
+        if (cnt > 0) {
+            const uint32_t u = draw_u31(kDomainPing, a.seed, uint32_t(a.tick), uint32_t(s), 0u, 0x100u);
+            const uint32_t rk = u % uint32_t(cnt);
+            const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
+            const int32_t g = __builtin_ffsll(own) - 1;
+            if (g == a.shard) {
+                if (!have_counts) {
+                    for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);
+                    uint32_t tot = 0;
+                    pre = wave_excl_prefix(lane_cnt, lane, &tot);
+                    have_counts = true;
+                }
+                const uint32_t local = rk - __shfl(cpre, g, 64);
+                const int32_t col = wave_select([&](int32_t w) { return bm[w]; }, per, lane_cnt, pre,
+                                                local, lane);
+                pick = int32_t(int64_t(a.shard) * a.stride + col);
+            }
+        }
+        if (lane == 0) a.picks[int64_t(s) * W + F] = pick;
     }
     if (lane == 0 && a.count_rounds && keff > 0)
         atomicAdd(&a.dig[(s % kDigSlots) * kDigFields + kDigSent], (unsigned long long)keff);
@@ -553,12 +576,14 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
 
 __global__ void scale_finalize_kernel(ScaleResolveArgs a) {
     const int64_t slots = int64_t(a.n) * a.fanout;
+    const int32_t W = a.fanout + (a.swim > 0 ? 1 : 0);
     unsigned long long dropped = 0;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < slots;
          i += int64_t(gridDim.x) * blockDim.x) {
-        int32_t d = a.picks[i];
+        const int32_t s = int32_t(i / a.fanout);
+        if (a.swim > 0 && i % a.fanout == 0) a.ping[s] = a.picks[int64_t(s) * W + a.fanout];
+        int32_t d = a.picks[int64_t(s) * W + (i - int64_t(s) * a.fanout)];
         if (d >= 0) {
-            const int32_t s = int32_t(i / a.fanout);
             const uint32_t dr = draw_u31(kDomainSend, a.seed, uint32_t(a.tick), uint32_t(s),
                                          uint32_t(d), 3u);
             if (int32_t(dr % 100u) < a.drop_pct) { dropped++; d = -1; }
@@ -685,14 +710,12 @@ hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st)
 template <bool kSlice, int kMerge>
 void launch_tick_policy(const ScaleTickArgs &a, int policy, size_t lds, hipStream_t st) {
     const dim3 grid(a.rows), block(kScaleBlock);
-    if constexpr (!kSlice) {
-        if (a.swim > 0) {
-            if (a.tfail > 0)
-                hipLaunchKernelGGL((scale_tick_kernel<false, false, kMerge, 1, false, true, true>), grid, block, lds, st, a);
-            else
-                hipLaunchKernelGGL((scale_tick_kernel<false, false, kMerge, 1, false, false, true>), grid, block, lds, st, a);
-            return;
-        }
+    if (a.swim > 0) {
+        if (a.tfail > 0)
+            hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, false, true, true>), grid, block, lds, st, a);
+        else
+            hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, false, false, true>), grid, block, lds, st, a);
+        return;
     }
     if (a.tfail > 0) {
         hipLaunchKernelGGL((scale_tick_kernel<false, kSlice, kMerge, 1, false, true>), grid, block, lds, st, a);

@@ -73,13 +73,16 @@ hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipS
 //   finalize (after an all-reduce MAX of picks): drop draw, out_dst, deg.
 struct ScaleResolveArgs {
     int32_t n, fanout, tick, drop_pct, shard, shards, count_rounds;
+    int32_t swim;                // SWIM probing: picks hold fanout + 1 slots per sender, the
+                                 // last one the probe target; finalize copies it to ping[]
     int64_t stride;              // slice width
     uint64_t seed;
     const int32_t *fail_tick;
     const int32_t *cnt_all;      // [shards][n]
     int32_t *cnt_total;          // [n]
     const uint8_t *bitmap;       // [n][stride / 8]
-    int32_t *picks;              // [n * fanout]
+    int32_t *picks;              // [n * (fanout + (swim > 0))]
+    int32_t *ping;               // swim: [n] probe target of each sender (or -1)
     int32_t *out_dst;            // [n * fanout]
     int32_t *deg;                // [n]
     unsigned long long *dig;

@@ -36,7 +36,7 @@ class ScaleEngine:
     tfail > 0: TFAIL suspicion (members tfail or more ticks stale are listed but not gossiped,
     chosen or counted); 0 is the reference's protocol.
     swim = s > 0: SWIM ping/ack probing, one probe target per node per tick over 1 direct + s - 1
-    indirect paths (answered: ts refreshed; unanswered: removed); fused or row layout only.
+    indirect paths (answered: ts refreshed; unanswered: removed); every layout.
     """
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,

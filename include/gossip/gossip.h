@@ -200,8 +200,8 @@ typedef struct {
     int32_t swim;       /* SWIM ping/ack probing (spec p.3, not in the reference): 0 off;
                            s = 1..8: each node probes one member per tick over 1 direct +
                            s - 1 indirect paths; answered -> ts refreshed, unanswered ->
-                           removed at the next tick (DESIGN.md "Scale mode").  Fused or
-                           row layout only                                             */
+                           removed at the next tick (DESIGN.md "Scale mode"); every
+                           layout                                                      */
 } gsp_scale_params;
 
 typedef struct {

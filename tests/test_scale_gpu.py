@@ -145,6 +145,9 @@ SWIM_CASES = [
     (CASES[2], 1, "columns", 1, 5, 2),
     (CASES[1], 3, "rows", 1, 0, 2),
     (CASES[3], 2, "rows", 1, 5, 1),
+    (CASES[1], 2, "columns", 1, 0, 2),
+    (CASES[3], 3, "columns", 0, 5, 1),
+    (CASES[4], 2, "columns", 1, 0, 3),
 ]
 
 
@@ -178,11 +181,6 @@ def test_swim_matches_oracle(case, shards, layout, merge, tfail, swim):
     assert differs, "probing changed nothing: the case does not exercise SWIM"
     orc.close()
     plain.close()
-
-
-def test_swim_rejects_column_shards():
-    with pytest.raises(Exception, match="swim"):
-        ScaleEngine(256, group=2, layout="columns", swim=1)
 
 
 def test_rccl_rank_path_one_rank():
