@@ -102,6 +102,7 @@ SIGNATURES = {
     "gsp_member_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspEntry), c_int32,
                                        P(c_int32)]),
     "gsp_write_msgcount": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, c_int32]),
+    "gsp_state_dump": (ctypes.c_int, [ctypes.c_void_p, c_int32, ctypes.c_char_p]),
     "gsp_counters": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), c_int32]),
     "gsp_flush_log": (ctypes.c_int, [ctypes.c_void_p]),
     "gsp_log_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,

@@ -13,6 +13,8 @@
 #include <cstring>
 #include <memory>
 #include <numeric>
+#include <set>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -33,18 +35,63 @@ struct NetMsg {
     int64_t send_batch;
 };
 
-// strcmp() over the two 6-byte addresses (EmulNet.cpp:154): the id bytes compared as a C
-// string, so e.g. ids 256 and 512 (both starting with a 0 byte) compare equal.
-bool addr_strcmp_equal(int32_t a, int32_t b) {
-    unsigned char x[5] = {0}, y[5] = {0};
-    std::memcpy(x, &a, 4);
-    std::memcpy(y, &b, 4);
+// strcmp() over the two 6-byte addresses (EmulNet.cpp:154) compares the little-endian id
+// bytes as a C string (the port bytes that follow are 0 for every node), so two ids match
+// iff their bytes agree up to the first 0 byte: e.g. ids 256 and 512 (first byte 0) match each
+// other, and 65537 matches 1.  addr_class(id) keeps exactly those bytes: equal classes <=>
+// strcmp() == 0.
+int32_t addr_class(int32_t id) {
+    const uint32_t u = uint32_t(id);
+    uint32_t out = 0;
     for (int i = 0; i < 4; ++i) {
-        if (x[i] != y[i]) return false;
-        if (x[i] == 0) return true;
+        const uint32_t b = (u >> (8 * i)) & 0xFFu;
+        if (!b) break;
+        out |= b << (8 * i);
     }
-    return true;  // continues into the port bytes, which are 0 for every node here
+    return int32_t(out);
 }
+
+// EmulNet's global message buffer (EmulNet.h:40, en_msg *buff[ENBUFFSIZE]) with its delivery
+// rule (EmulNet.cpp:151-161): ENrecv scans the buffer top-down and takes every message whose
+// destination address strcmp-matches the receiver, moving the current last message into the
+// hole.  Messages that linger (e.g. to a failed node) keep taking part in that permutation.
+// The same permutation in O(matches * log |B|) instead of O(|B|) per receiver: the buffer
+// positions of every address class are kept in an ordered set.  Scanning top-down takes the
+// class's positions in descending order; when position k is taken, every position above k
+// holds a message of another class (the class's larger positions were taken first and only
+// other classes' messages are moved down), so the message moved from the end into k belongs
+// to another class and the class's remaining positions are unchanged.
+class EmulBuffer {
+  public:
+    size_t size() const { return msgs_.size(); }
+    void push(const NetMsg &m) {
+        pos_[addr_class(m.dst)].insert(int32_t(msgs_.size()));
+        msgs_.push_back(m);
+    }
+    template <typename F>
+    void deliver(int32_t id, F &&take) {
+        auto it = pos_.find(addr_class(id));
+        if (it == pos_.end()) return;
+        std::set<int32_t> &mine = it->second;
+        while (!mine.empty()) {
+            const int32_t k = *mine.rbegin();
+            mine.erase(std::prev(mine.end()));
+            take(msgs_[size_t(k)]);
+            const int32_t last = int32_t(msgs_.size()) - 1;
+            if (last != k) {
+                std::set<int32_t> &other = pos_[addr_class(msgs_[size_t(last)].dst)];
+                other.erase(last);
+                other.insert(k);
+                msgs_[size_t(k)] = msgs_[size_t(last)];
+            }
+            msgs_.pop_back();
+        }
+    }
+
+  private:
+    std::vector<NetMsg> msgs_;
+    std::unordered_map<int32_t, std::set<int32_t>> pos_;
+};
 
 }  // namespace
 
@@ -60,7 +107,7 @@ struct gsp_engine {
     int64_t draws = 0;
     int64_t batch_seq = 1;
 
-    std::vector<NetMsg> buf;                  // EmulNet::emulnet.buff
+    EmulBuffer buf;                           // EmulNet::emulnet.buff
     std::vector<std::vector<NetMsg>> queue;   // Member::mp1q per node
     std::vector<int8_t> failed;
     std::vector<int64_t> last_commit;
@@ -252,14 +299,10 @@ int gsp_tick_recv(gsp_engine *e, int32_t tick, const int32_t *order, int32_t n) 
         const int32_t node = order[i];
         GSP_REQUIRE(node >= 0 && node < e->n, GSP_ERR_INVALID, "gsp_tick_recv: node %d", node);
         const int32_t id = node + 1;
-        auto &b = e->buf;
-        for (int64_t k = int64_t(b.size()) - 1; k >= 0; --k) {   // EmulNet.cpp:151-173
-            if (!addr_strcmp_equal(b[size_t(k)].dst, id)) continue;
-            e->queue[node].push_back(b[size_t(k)]);
-            b[size_t(k)] = b.back();
-            b.pop_back();
+        e->buf.deliver(id, [&](const NetMsg &m) {             // EmulNet.cpp:151-173
+            e->queue[node].push_back(m);
             e->recv_ctr[size_t(id) * kMaxTicks + tick]++;
-        }
+        });
     }
     return GSP_OK;
 }
@@ -414,7 +457,7 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         }
     }
     for (int32_t k = 0; k < n_adm; ++k)
-        e->buf.push_back(NetMsg{a_src[k], a_dst[k], a_type[k], e->batch_seq});
+        e->buf.push(NetMsg{a_src[k], a_dst[k], a_type[k], e->batch_seq});
     for (int32_t i = 0; i < n; ++i) {
         const int32_t node = h_node[i];
         e->inited[node] = o_state[size_t(i) * 4 + 0];
@@ -458,7 +501,7 @@ int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int3
         kMsgHdrBytes + kEnMsgBytes >= e->p.max_msg_size || (dropmsg && draw % 100 < thr))
         return GSP_OK;
     // the payload of a GOSSIP is the sender's list as committed now
-    e->buf.push_back(NetMsg{src_id, dst_id, type, e->last_commit[src_node]});
+    e->buf.push(NetMsg{src_id, dst_id, type, e->last_commit[src_node]});
     e->sent_host[size_t(src_id) * kMaxTicks + tick]++;
     e->stats.sends_admitted++;
     *admitted = kMsgHdrBytes;
@@ -525,6 +568,52 @@ int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, in
     }
     *n = cnt;
     for (int32_t k = 0; k < cnt && k < cap; ++k) buf[k] = list[k];
+    return GSP_OK;
+}
+
+// Every node's state after tick `tick`, appended to `path` as one line per node in id order:
+//   t id inited inGroup bFailed heartbeat |L| id:hb:ts ...      (list in MemberListEntry order)
+// -- the Member fields the reference keeps (Member.h:89-122), in the end-of-tick dump format
+// of the parity fixtures (oracle/ref_hooks.cpp).  One copy of the device tables per call.
+int gsp_state_dump(gsp_engine *e, int32_t tick, const char *path) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(path, GSP_ERR_INVALID, "gsp_state_dump: NULL path");
+    const int32_t N = e->n;
+    const size_t nn = size_t(N) * N;
+    std::vector<int64_t> key(nn);
+    std::vector<int32_t> hb(nn), ts(nn), rank(nn);
+    GSP_HIP(hipMemcpyAsync(key.data(), e->t_key.p, nn * 8, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(hb.data(), e->t_hb.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(ts.data(), e->t_ts.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(rank.data(), e->t_rank.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    FILE *f = std::fopen(path, "a");
+    GSP_REQUIRE(f, GSP_ERR_IO, "gsp_state_dump: cannot open %s", path);
+    std::vector<int32_t> order(static_cast<size_t>(N));
+    std::string line;
+    char tmp[64];
+    for (int32_t node = 0; node < N; ++node) {
+        const size_t row = size_t(node) * N;
+        int32_t cnt = 0;
+        for (int32_t x = 0; x < N; ++x) {
+            if (key[row + x] < 0) continue;
+            const int32_t rk = rank[row + x];
+            if (rk < 0 || rk >= N) { std::fclose(f); GSP_REQUIRE(false, GSP_ERR_INVALID, "corrupt rank"); }
+            order[size_t(rk)] = x;
+            cnt++;
+        }
+        std::snprintf(tmp, sizeof tmp, "%d %d %d %d %d %d %d", tick, node + 1, e->inited[node],
+                      e->in_group[node], int(e->failed[node]), e->own_hb[node], cnt);
+        line = tmp;
+        for (int32_t k = 0; k < cnt; ++k) {
+            const int32_t x = order[size_t(k)];
+            std::snprintf(tmp, sizeof tmp, " %d:%d:%d", x + 1, hb[row + x], ts[row + x]);
+            line += tmp;
+        }
+        line += '\n';
+        std::fwrite(line.data(), 1, line.size(), f);
+    }
+    std::fclose(f);
     return GSP_OK;
 }
 

@@ -69,6 +69,8 @@ struct gsp_pview {
     int32_t tick = 0;
     bool timing = true;
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
+    int32_t max_segment = gsp::kPvMaxSegment;
+    int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail;
     int32_t *h_cnt = nullptr;    // pinned [G][2G]: pair counts then record counts per shard
@@ -116,6 +118,7 @@ struct gsp_pview {
         a.deg = sh.deg.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
         a.err = sh.err.p;
+        a.max_segment = max_segment;
         a.prof = sh.prof.p;
         a.waves = waves;
         return a;
@@ -129,6 +132,8 @@ struct gsp_pview {
         a.rows = sh.rows;
         a.row0 = sh.row0;
         a.inbox = p.inbox;
+        a.tick = tick + 1;
+        a.max_segment = max_segment;
         a.rc_info = sh.rc_info.p;
         a.rc_src = sh.rc_src.p;
         a.rc_slot = sh.rc_slot.p;
@@ -215,6 +220,17 @@ int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
     return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
 }
 
+// The capacity flags as last mirrored to the host: a receiver sent more than max_segment
+// messages at tick t sets its shard's flag to t, and the tick kernels of t and every later
+// tick run no row, so the job's state stays that of tick t - 1.
+int pview_mirrored_err(gsp_pview *s) {
+    for (size_t i = 0; i < s->local.size(); ++i)
+        GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
+                    "a receiver was sent more than %d messages at tick %d; the job stopped there",
+                    s->max_segment, s->h_err[i]);
+    return GSP_OK;
+}
+
 int pview_collect(gsp_pview *s) {
     for (auto &t : s->pending) {
         float a = 0.f, b = 0.f;
@@ -229,12 +245,9 @@ int pview_collect(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     s->pending.clear();
-    for (PvShard &sh : s->local) {
-        int32_t err = 0;
-        GSP_HIP(hipMemcpy(&err, sh.err.p, 4, hipMemcpyDeviceToHost));
-        GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY, "a receiver got more than 1024 messages in one tick");
-    }
-    return GSP_OK;
+    for (size_t i = 0; i < s->local.size(); ++i)
+        GSP_HIP(hipMemcpy(s->h_err + i, s->local[i].err.p, 4, hipMemcpyDeviceToHost));
+    return pview_mirrored_err(s);
 }
 
 int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t rank,
@@ -265,7 +278,11 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         max_rows = std::max(max_rows, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
     s->pair_cap = max_rows;                       // a sender row goes to a shard at most once
     s->msg_cap = int64_t(max_rows) * p->fanout;
+    if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
+        s->max_segment = std::max(1, std::min(gsp::kPvMaxSegment, std::atoi(ms)));
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
+    std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
@@ -348,6 +365,7 @@ int gsp_pview_destroy(gsp_pview *s) {
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_recv) (void)hipHostFree(s->h_recv);
+    if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -357,6 +375,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
     GSP_REQUIRE(s && ticks >= 0, GSP_ERR_INVALID, "gsp_pview_step: bad argument");
     GSP_REQUIRE(s->tick + ticks <= s->p.max_ticks, GSP_ERR_RANGE, "gsp_pview_step: beyond max_ticks");
     GSP_HIP(hipSetDevice(s->device));
+    if (int rc = pview_mirrored_err(s)) return rc;   // an earlier call's ticks overflowed
     const int32_t n = s->p.n;
     for (int32_t i = 0; i < ticks; ++i) {
         const int32_t t = s->tick + 1;
@@ -385,6 +404,8 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         s->tick = t;
         s->perf.ticks++;
     }
+    for (size_t i = 0; i < s->local.size(); ++i)     // read by the next call, never waited on
+        GSP_HIP(hipMemcpyAsync(s->h_err + i, s->local[i].err.p, 4, hipMemcpyDeviceToHost, s->st));
     return GSP_OK;
 }
 

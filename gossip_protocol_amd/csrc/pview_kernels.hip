@@ -607,9 +607,9 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
         my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
         my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
     }
-    if (a.tick > a.fail_tick[r]) {          // crashed: no recv, no ops, no send
-        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
-        return;
+    if (a.tick > a.fail_tick[r] || (!kInit && *a.err)) {   // crashed (no recv, no ops, no
+        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;  // send), or a capacity error
+        return;                                                 // stopped the job
     }
 
     PvMark pm;
@@ -644,10 +644,6 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
         // ---- 1. receipt record (loaded above), read by every wave -----------------------------
         k = info & 7;
         k_all = info >> 3;
-        if (k_all > kPvMaxSegment) {        // flagged by the receipt kernel
-            if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
-            return;
-        }
         uint32_t ssrc[kPvMaxInbox];
         int32_t sslot[kPvMaxInbox];
 #pragma unroll
@@ -680,8 +676,8 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
     int32_t bs[8], bl[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
-    if (k_all > kPvMaxSegment) {
-        atomicOr(a.err, 1);
+    if (k_all > a.max_segment) {
+        atomicCAS(a.err, 0, a.tick);        // this tick's tick kernel sees it and runs no row
     } else {
         for (int32_t i = 0; i < k_all; ++i) {             // insertion into the sorted best 8
             int32_t s = a.csr_src[o0 + i];
@@ -704,7 +700,7 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
     ps[1] = make_int4(bs[4], bs[5], bs[6], bs[7]);
     pl[0] = make_int4(bl[0], bl[1], bl[2], bl[3]);
     pl[1] = make_int4(bl[4], bl[5], bl[6], bl[7]);
-    a.rc_info[lr] = (k_all > kPvMaxSegment ? 0 : k) | (k_all << 3);
+    a.rc_info[lr] = (k_all > a.max_segment ? 0 : k) | (k_all << 3);
 }
 
 // Peers and sends of every row (one lane per row), after the tick kernel wrote the views:
@@ -715,8 +711,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     const int32_t r = a.row0 + lr, F = a.fanout;
     const uint32_t t = uint32_t(a.tick);
     unsigned long long *w3 = a.rowdig + int64_t(lr) * 16 + 3;
-    bool dead = a.tick > a.fail_tick[r];
-    if (!dead && a.tick > 0) dead = (a.rc_info[lr] >> 3) > kPvMaxSegment;
+    const bool dead = a.tick > a.fail_tick[r] || (a.tick > 0 && *a.err);
     int32_t *od = a.out_dst + int64_t(lr) * F;
     if (dead) {
         for (int32_t q = 0; q < F; ++q) od[q] = -1;

@@ -40,7 +40,9 @@ struct PviewTickArgs {
     int32_t *deg;                // [n]
     unsigned long long *rowdig;  // [rows][4][4] per-row digest records of this tick
     unsigned long long *dig;     // [kPvDigSlots][kPvFields] of this tick
-    int32_t *err;
+    int32_t *err;                // [1] capacity error: 0, else the first tick a receiver was
+                                 // sent more than max_segment messages (the job stops there)
+    int32_t max_segment;         // <= kPvMaxSegment (lowered only by tests)
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
     int32_t waves;               // register budget variant of the tick kernel (7 or 8)
 };
@@ -50,7 +52,7 @@ struct PviewReceiptArgs {
     const int32_t *off;          // [rows + 1] receiver CSR
     const int32_t *csr_src;      // sender ids
     const int32_t *csr_slot;     // row mode: sender rows (null: local row = src - row0)
-    int32_t rows, row0, inbox;
+    int32_t rows, row0, inbox, tick, max_segment;
     int32_t *rc_info, *rc_src, *rc_slot;
     int32_t *err;
 };

@@ -61,6 +61,9 @@ struct gsp_scale {
     bool rowmode = false;      // row layout (G > 1): sender rows move between shards
     int64_t pair_cap = 0, msg_cap = 0;
     int32_t *h_cnt = nullptr, *h_recv = nullptr;   // pinned exchange counts (row layout)
+    int32_t *h_err = nullptr;  // pinned mirror of the shards' capacity flags, refreshed by an
+                               // async copy at the end of every gsp_scale_step call
+    int32_t max_segment = gsp::kMaxSegment;
     ncclComm_t comm = nullptr; // one shard per process when set
     int64_t width = 0;         // n rounded up to 2048 * G
     int64_t stride = 0;        // columns per shard
@@ -121,6 +124,7 @@ struct gsp_scale {
         a.bitmap = sh.bitmap.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
+        a.max_segment = max_segment;
         return a;
     }
 
@@ -319,15 +323,22 @@ int exchange_rows(gsp_scale *s, int32_t t_sent) {
     return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
 }
 
-int check_err(gsp_scale *s) {
-    for (Shard &sh : s->local) {
-        int32_t err = 0;
-        GSP_HIP(hipMemcpyAsync(&err, sh.err.p, 4, hipMemcpyDeviceToHost, s->st));
-        GSP_HIP(hipStreamSynchronize(s->st));
-        GSP_REQUIRE(err == 0, GSP_ERR_CAPACITY, "a receiver got more than %d messages in one tick",
-                    gsp::kMaxSegment);
-    }
+// The capacity flags as last mirrored to the host (no synchronisation): a receiver with more
+// than max_segment messages sets its shard's flag to the tick, and every later tick kernel
+// returns at once, so the job's state stays that of the tick before the overflow.
+int mirrored_err(gsp_scale *s) {
+    for (size_t i = 0; i < s->local.size(); ++i)
+        GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
+                    "a receiver got more than %d messages at tick %d; ticks after it did not run",
+                    s->max_segment, s->h_err[i]);
     return GSP_OK;
+}
+
+int check_err(gsp_scale *s) {
+    for (size_t i = 0; i < s->local.size(); ++i)
+        GSP_HIP(hipMemcpyAsync(s->h_err + i, s->local[i].err.p, 4, hipMemcpyDeviceToHost, s->st));
+    GSP_HIP(hipStreamSynchronize(s->st));
+    return mirrored_err(s);
 }
 
 int collect_timing(gsp_scale *s) {
@@ -393,7 +404,11 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                     "row bitmap of %lld B exceeds the LDS budget (one-GPU full view n <= 393216)",
                     (long long)(s->stride / 8));
     }
+    if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
+        s->max_segment = std::max(1, std::min(gsp::kMaxSegment, std::atoi(ms)));
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+    GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
+    std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
@@ -474,6 +489,7 @@ int gsp_scale_destroy(gsp_scale *s) {
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_recv) (void)hipHostFree(s->h_recv);
+    if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -484,6 +500,7 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
     GSP_REQUIRE(s->tick + ticks <= s->p.max_ticks, GSP_ERR_RANGE,
                 "gsp_scale_step: tick %d beyond max_ticks %d", s->tick + ticks, s->p.max_ticks);
     GSP_HIP(hipSetDevice(s->device));
+    if (int rc = mirrored_err(s)) return rc;     // an earlier call's ticks overflowed
     const int32_t n = s->p.n;
     const int64_t slots = int64_t(n) * s->p.fanout;
     for (int32_t i = 0; i < ticks; ++i) {
@@ -518,6 +535,8 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
         s->tick = t;
         s->perf.ticks++;
     }
+    for (size_t i = 0; i < s->local.size(); ++i)     // read by the next call, never waited on
+        GSP_HIP(hipMemcpyAsync(s->h_err + i, s->local[i].err.p, 4, hipMemcpyDeviceToHost, s->st));
     return GSP_OK;
 }
 

@@ -206,6 +206,7 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     const int32_t t = a.tick;
     const int32_t F = a.fanout;
 
+    if (!kInit && *a.err) return;      // a capacity error froze the job at an earlier tick
     if (t > a.fail_tick[r]) {          // crashed (Application.cpp:186): no recv, no ops, no send
         if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
         return;
@@ -215,8 +216,8 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     if (!kInit) {
         const int32_t o0 = a.off[lr];
         k = a.off[lr + 1] - o0;
-        if (k > kMaxSegment) {
-            if (tid == 0) atomicOr(a.err, 1);
+        if (k > a.max_segment) {
+            if (tid == 0) atomicCAS(a.err, 0, t);
             if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
             return;
         }

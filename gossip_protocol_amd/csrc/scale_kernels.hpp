@@ -59,7 +59,9 @@ struct ScaleTickArgs {
     int32_t *ping;               // swim: [rows] probe target of the last send (-1 none)
     uint8_t *bitmap;             // slice mode: [rows][stride / 8] presence bits
     unsigned long long *dig;     // [kDigSlots][kDigFields] of this tick
-    int32_t *err;                // [1] capacity error flag
+    int32_t *err;                // [1] capacity error: 0, else the first tick a receiver got
+                                 // more than max_segment messages (every later tick is a no-op)
+    int32_t max_segment;         // <= kMaxSegment (lowered only by tests, GSP_TEST_MAX_SEGMENT)
 };
 
 // merge: 0 = per-entry scalar form, 1 = packed 16-bit form (v_pk_* / v_bfi_b32)

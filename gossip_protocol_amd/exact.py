@@ -75,6 +75,9 @@ class Engine:
               "gsp_member_list")
         return [(buf[i].id, buf[i].heartbeat, buf[i].timestamp) for i in range(cnt.value)]
 
+    def state_dump(self, tick, path):
+        check(lib().gsp_state_dump(self._h, tick, path.encode()), "gsp_state_dump")
+
     def write_msgcount(self, path, tick):
         check(lib().gsp_write_msgcount(self._h, path.encode(), tick), "gsp_write_msgcount")
 
@@ -99,7 +102,9 @@ def run_application(conf_path, seed, rng="glibc", out_dir=".", device=0, ticks=N
     T = p.total_running_time if ticks is None else ticks
     os.makedirs(out_dir, exist_ok=True)
     dbg = os.path.join(out_dir, "dbg.log")
-    state_lines = []
+    state_path = os.path.join(out_dir, "state.txt")
+    if state_dump and os.path.exists(state_path):
+        os.remove(state_path)
     stdout_lines = []
     failed = [False] * n
     dropmsg = 0
@@ -141,17 +146,9 @@ def run_application(conf_path, seed, rng="glibc", out_dir=".", device=0, ticks=N
             if p.drop_msg and t == 300:
                 dropmsg = 0
             if state_dump:
-                for i in range(n):
-                    m = e.member(i)
-                    lst = e.member_list(i)
-                    state_lines.append("%d %d %d %d %d %d %d%s" % (
-                        t, i + 1, m.inited, m.in_group, int(failed[i]), m.heartbeat, len(lst),
-                        "".join(" %d:%d:%d" % x for x in lst)))
+                e.state_dump(t, state_path)
         e.write_msgcount(os.path.join(out_dir, "msgcount.log"), T)
         stats = e.stats()
-    if state_dump:
-        with open(os.path.join(out_dir, "state.txt"), "w") as f:
-            f.write("".join(l + "\n" for l in state_lines))
     with open(os.path.join(out_dir, "stdout.txt"), "w") as f:
         f.write("".join(l + "\n" for l in stdout_lines))
     return {"dbg.log": dbg, "msgcount.log": os.path.join(out_dir, "msgcount.log"),

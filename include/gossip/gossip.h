@@ -158,6 +158,12 @@ int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out);
 /* The member list of `node` in list order (MemberListEntry vector order). */
 int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n);
 
+/* Every node's end-of-tick state appended to `path`, one line per node in id order:
+ * "t id inited inGroup bFailed heartbeat |L| id:hb:ts ..." with the list in MemberListEntry
+ * order (Member.h:89-122) -- the state format of the parity fixtures.  bFailed is the flag set
+ * by gsp_set_failed (Application::fail, Application.cpp:186/194). */
+int gsp_state_dump(gsp_engine *e, int32_t tick, const char *path);
+
 /* EmulNet::ENcleanup (EmulNet.cpp:184-220): writes msgcount.log for ticks [0, tick). */
 int gsp_write_msgcount(gsp_engine *e, const char *path, int32_t tick);
 /* Per-(node, tick) counters: sent[(id) * ticks + t], recv likewise, id in 1..N. */

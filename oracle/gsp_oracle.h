@@ -109,5 +109,17 @@ int gsp_pview_oracle_own_hb(const gsp_pview_oracle *o, int32_t r);
 int32_t gsp_pview_oracle_fail_tick(const gsp_pview_oracle *o, int32_t r);
 int64_t gsp_pview_oracle_messages(const gsp_pview_oracle *o, int32_t *src, int32_t *dst,
                                   int64_t cap);
+/* The per-row rule of gsp_pview_oracle_step for ONE alive row r at tick t, on views the caller
+ * hands in (ids ascending, absolute ts): own view, the ids that sent to r at t - 1 (any order
+ * and count: sorted, the first `inbox` merged, the rest counted as overflow) and their views
+ * (`view` slots each, in the order of `senders`).  Writes r's view of tick t, returns its
+ * length; adds the row's counts / event hashes to *d (node_rounds += 1). */
+int32_t gsp_pview_oracle_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r,
+                                  const int32_t *own_id, const int32_t *own_hb,
+                                  const int32_t *own_ts, int32_t own_len, int32_t nsend,
+                                  const int32_t *senders, const int32_t *sv_id,
+                                  const int32_t *sv_hb, const int32_t *sv_ts,
+                                  const int32_t *sv_len, int32_t *out_id, int32_t *out_hb,
+                                  int32_t *out_ts, gsp_pview_digest *d);
 
 #endif

@@ -29,6 +29,7 @@ typedef struct {
     int src, dst, type;
     entry_t *payload; /* GOSSIP: copy of the sender's list at send time (MP1Node.cpp:357) */
     int npayload;
+    int dkey;         /* addr_key(dst): the destination address as strcmp() sees it */
 } msg_t;
 
 typedef struct {
@@ -101,13 +102,32 @@ static int draw_fail(sim_t *s) {
     return gsp_glibc_rand(&s->glibc);
 }
 
+/* strcmp() over the 6-byte addresses (EmulNet.cpp:154) is C-string equality of the
+ * little-endian id bytes followed by the port bytes (port 0 here): two addresses compare equal
+ * iff their id bytes agree up to the first 0 byte.  addr_key keeps exactly those bytes, so the
+ * buffer scan compares one int per message (equal keys <=> strcmp() == 0; e.g. ids 256 and
+ * 512 share the key 0). */
+static int addr_key(int id) {
+    unsigned char x[7] = {0};
+    memcpy(x, &id, 4);
+    int key = 0;
+    for (int i = 0; i < 4 && x[i]; ++i) key |= (int)x[i] << (8 * i);
+    return key;
+}
+
+/* sends the last gsp_oracle_mp1_run rejected because the 30,000-message buffer was full
+ * (EmulNet.cpp:92): lets the fixture tests show that a case reaches that path */
+static int64_t g_buffer_full_rejects;
+int64_t gsp_oracle_mp1_buffer_full_rejects(void) { return g_buffer_full_rejects; }
+
 /* ---------------- EmulNet (EmulNet.cpp) ---------------- */
 static void en_send(sim_t *s, int src_node, int dst_id, int type, const entry_t *pl, int npl) {
     s->cur_src = src_node + 1; s->cur_dst = dst_id; s->cur_type = type;
     int r = draw_send(s);                                  /* EmulNet.cpp:89, always drawn */
     int thr = (int)(s->drop_prob * 100);                   /* EmulNet.cpp:91               */
-    if (s->nbuf >= EN_BUFF_CAP || (s->dropmsg && r % 100 < thr)) return;
-    msg_t m = {src_node + 1, dst_id, type, NULL, 0};
+    if (s->nbuf >= EN_BUFF_CAP) { g_buffer_full_rejects++; return; }   /* EmulNet.cpp:92 */
+    if (s->dropmsg && r % 100 < thr) return;
+    msg_t m = {src_node + 1, dst_id, type, NULL, 0, addr_key(dst_id)};
     if (type == M_GOSSIP && npl) {
         m.payload = malloc(sizeof(entry_t) * npl);
         memcpy(m.payload, pl, sizeof(entry_t) * npl);
@@ -117,18 +137,11 @@ static void en_send(sim_t *s, int src_node, int dst_id, int type, const entry_t 
     s->sent[(src_node + 1) * MAX_TICKS + s->t]++;          /* EmulNet.cpp:110 */
 }
 
-/* strcmp() over the 6-byte addresses (EmulNet.cpp:154): C-string equality of the
- * little-endian id bytes followed by the port bytes (port 0 here). */
-static int addr_strcmp_eq(int a, int b) {
-    unsigned char x[7] = {0}, y[7] = {0};
-    memcpy(x, &a, 4); memcpy(y, &b, 4);
-    return strcmp((const char *)x, (const char *)y) == 0;
-}
-
 static void en_recv(sim_t *s, int node) {
     node_t *nd = &s->nodes[node];
+    const int key = addr_key(node + 1);
     for (int k = s->nbuf - 1; k >= 0; --k) {               /* EmulNet.cpp:151 top-down scan */
-        if (!addr_strcmp_eq(s->buf[k].dst, node + 1)) continue;
+        if (s->buf[k].dkey != key) continue;               /* EmulNet.cpp:154 strcmp() */
         if (nd->nqueue == nd->cap) {
             nd->cap = nd->cap ? nd->cap * 2 : 16;
             nd->queue = realloc(nd->queue, sizeof(msg_t) * nd->cap);
@@ -298,6 +311,7 @@ int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int t
                        const char *stdout_path) {
     sim_t s;
     memset(&s, 0, sizeof s);
+    g_buffer_full_rejects = 0;
     if (read_conf(&s, conf_path) != 0) return -1;
     if (s.n <= 0 || s.n > 1000 || ticks <= 0 || ticks > MAX_TICKS) return -2;
     s.rng_mode = rng_mode;

@@ -176,9 +176,122 @@ static int cmp_id(const void *a, const void *b) {
     return (x->id > y->id) - (x->id < y->id);
 }
 
+/* One alive receiver's tick t: merge the views of the (ascending, at most K) senders `b` into
+ * its own view (prev = the views of tick t - 1, sorted by id), TREMOVE scan, eviction to V.
+ * Writes the new view to out (sorted by id) and returns its length; adds the row's counts and
+ * event hashes to *d.  Scratch: ids / res / kk of V + K (V + 1) + 1 entries each. */
+static int32_t pv_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r, const pv_ent *own,
+                           int32_t own_len, int32_t k, const int32_t *b, const pv_ent *const *sv,
+                           const int32_t *slen, pv_ent *out, gsp_pview_digest *d, int32_t *ids,
+                           pv_ent *res, keyed *kk) {
+    const int32_t V = c->view, T = c->tremove;
+    d->delivered += k;
+    /* candidate ids: own view, each sender, each payload */
+    int32_t nid = 0;
+    for (int32_t i = 0; i < own_len; ++i) ids[nid++] = own[i].id;
+    for (int32_t j = 0; j < k; ++j) {
+        ids[nid++] = b[j];
+        for (int32_t i = 0; i < slen[j]; ++i) ids[nid++] = sv[j][i].id;
+        d->merges += 1 + slen[j];
+    }
+    qsort(ids, nid, sizeof(int32_t), cmp_i32);
+    int32_t nres = 0;
+    for (int32_t i = 0; i < nid; ++i) {
+        if (i && ids[i] == ids[i - 1]) continue;
+        const int32_t x = ids[i];
+        const pv_ent *e0 = find_id(own, own_len, x);
+        int present = e0 != NULL;
+        pv_ent cur = e0 ? *e0 : (pv_ent){x, 0, 0};
+        for (int32_t j = 0; j < k; ++j) {
+            const int32_t s = b[j];
+            if (x == s) {                                   /* MP1Node.cpp:237-243 */
+                if (present) { cur.hb += 1; cur.ts = t; }
+                else { present = 1; cur.hb = 1; cur.ts = t; }
+                continue;
+            }
+            const pv_ent *v = find_id(sv[j], slen[j], x);
+            if (!v) continue;
+            if (present) {                                  /* MP1Node.cpp:247-251 */
+                if (v->hb > cur.hb) { cur.hb = v->hb; cur.ts = t; }
+            } else if (x != r && t - v->ts < T) {           /* MP1Node.cpp:282-301 */
+                present = 1; cur.hb = v->hb; cur.ts = v->ts;
+            }
+        }
+        if (!present) continue;
+        if (!e0) { d->joins++; d->event_hash += gsp_pv_event_mix(1, t, r, x); }
+        if (t - cur.ts >= T) {                              /* MP1Node.cpp:340 */
+            d->removes++; d->event_hash += gsp_pv_event_mix(2, t, r, x);
+            continue;
+        }
+        res[nres++] = cur;
+    }
+    if (nres > V) {
+        for (int32_t i = 0; i < nres; ++i) { kk[i].e = res[i]; kk[i].age = t - res[i].ts; }
+        qsort(kk, nres, sizeof(keyed), cmp_keep);
+        for (int32_t i = V; i < nres; ++i) {
+            d->evicts++;
+            d->event_hash += gsp_pv_event_mix(3, t, r, kk[i].e.id);
+        }
+        for (int32_t i = 0; i < V; ++i) res[i] = kk[i].e;
+        nres = V;
+        qsort(res, nres, sizeof(pv_ent), cmp_id);
+    }
+    memcpy(out, res, sizeof(pv_ent) * nres);
+    return nres;
+}
+
+/* The per-row rule above for ONE row, on views handed in by the caller (ids ascending, ts
+ * absolute): tests recompute a sampled row of a full-size GPU run from the previous tick's
+ * views and the message list.  senders: the ids that sent to r at t - 1 (any order, any
+ * count: sorted here, the first K merged, the rest inbox overflow); sv_*: their views, V
+ * slots each, in the order of `senders`.  Returns the new length (or -1). */
+int32_t gsp_pview_oracle_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r,
+                                  const int32_t *own_id, const int32_t *own_hb,
+                                  const int32_t *own_ts, int32_t own_len, int32_t nsend,
+                                  const int32_t *senders, const int32_t *sv_id,
+                                  const int32_t *sv_hb, const int32_t *sv_ts,
+                                  const int32_t *sv_len, int32_t *out_id, int32_t *out_hb,
+                                  int32_t *out_ts, gsp_pview_digest *d) {
+    const int32_t V = c->view, K = c->inbox;
+    if (nsend < 0 || own_len < 0 || own_len > V) return -1;
+    int32_t *order = malloc(sizeof(int32_t) * (nsend ? nsend : 1));
+    for (int32_t j = 0; j < nsend; ++j) order[j] = j;
+    for (int32_t i = 1; i < nsend; ++i) {                  /* ascending sender id */
+        int32_t v = order[i], j = i - 1;
+        while (j >= 0 && senders[order[j]] > senders[v]) { order[j + 1] = order[j]; j--; }
+        order[j + 1] = v;
+    }
+    const int32_t k = nsend < K ? nsend : K;
+    d->overflow += nsend - k;
+    pv_ent *own = malloc(sizeof(pv_ent) * (V ? V : 1));
+    pv_ent *views = malloc(sizeof(pv_ent) * (size_t)(k ? k : 1) * V);
+    const pv_ent **sv = malloc(sizeof(pv_ent *) * (k ? k : 1));
+    int32_t *b = malloc(sizeof(int32_t) * (k ? k : 1)), *slen = malloc(sizeof(int32_t) * (k ? k : 1));
+    for (int32_t i = 0; i < own_len; ++i) own[i] = (pv_ent){own_id[i], own_hb[i], own_ts[i]};
+    for (int32_t j = 0; j < k; ++j) {
+        const int32_t q = order[j];
+        b[j] = senders[q];
+        slen[j] = sv_len[q];
+        for (int32_t i = 0; i < sv_len[q]; ++i)
+            views[(size_t)j * V + i] = (pv_ent){sv_id[(size_t)q * V + i], sv_hb[(size_t)q * V + i],
+                                                 sv_ts[(size_t)q * V + i]};
+        sv[j] = views + (size_t)j * V;
+    }
+    const size_t cap = (size_t)V + (size_t)K * (V + 1) + 1;
+    int32_t *ids = malloc(sizeof(int32_t) * cap);
+    pv_ent *res = malloc(sizeof(pv_ent) * cap), *out = malloc(sizeof(pv_ent) * (V ? V : 1));
+    keyed *kk = malloc(sizeof(keyed) * cap);
+    d->node_rounds++;
+    const int32_t m = pv_row_step(c, t, r, own, own_len, k, b, sv, slen, out, d, ids, res, kk);
+    for (int32_t i = 0; i < m; ++i) { out_id[i] = out[i].id; out_hb[i] = out[i].hb; out_ts[i] = out[i].ts; }
+    free(order); free(own); free(views); free(sv); free(b); free(slen); free(ids); free(res);
+    free(out); free(kk);
+    return m;
+}
+
 int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
     const gsp_pview_cfg *c = &o->c;
-    const int32_t n = c->n, V = c->view, T = c->tremove, K = c->inbox;
+    const int32_t n = c->n, V = c->view, K = c->inbox;
     const int32_t t = o->t + 1;
     const int prev = o->cur, next = 1 - o->cur;
     memset(d, 0, sizeof *d);
@@ -196,6 +309,8 @@ int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
     int32_t *ids = malloc(sizeof(int32_t) * (size_t)(V + (size_t)K * (V + 1) + 1));
     pv_ent *res = malloc(sizeof(pv_ent) * (size_t)(V + (size_t)K * (V + 1) + 1));
     keyed *kk = malloc(sizeof(keyed) * (size_t)(V + (size_t)K * (V + 1) + 1));
+    const pv_ent **sv = malloc(sizeof(pv_ent *) * (size_t)K);
+    int32_t *slen = malloc(sizeof(int32_t) * (size_t)K);
 
     for (int32_t r = 0; r < n; ++r) {
         pv_ent *out = o->tab[next] + (size_t)r * V;
@@ -211,64 +326,15 @@ int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
         int32_t k = deg[r + 1] - deg[r];
         qsort(b, k, sizeof(int32_t), cmp_i32);
         if (k > K) { d->overflow += k - K; k = K; }
-        d->delivered += k;
-        /* candidate ids: own view, each sender, each payload */
-        int32_t nid = 0;
-        for (int32_t i = 0; i < own_len; ++i) ids[nid++] = own[i].id;
         for (int32_t j = 0; j < k; ++j) {
-            int32_t s = b[j];
-            ids[nid++] = s;
-            const pv_ent *pl = o->tab[prev] + (size_t)s * V;
-            for (int32_t i = 0; i < o->len[prev][s]; ++i) ids[nid++] = pl[i].id;
-            d->merges += 1 + o->len[prev][s];
+            sv[j] = o->tab[prev] + (size_t)b[j] * V;
+            slen[j] = o->len[prev][b[j]];
         }
-        qsort(ids, nid, sizeof(int32_t), cmp_i32);
-        int32_t nres = 0;
-        for (int32_t i = 0; i < nid; ++i) {
-            if (i && ids[i] == ids[i - 1]) continue;
-            const int32_t x = ids[i];
-            const pv_ent *e0 = find_id(own, own_len, x);
-            int present = e0 != NULL;
-            pv_ent cur = e0 ? *e0 : (pv_ent){x, 0, 0};
-            for (int32_t j = 0; j < k; ++j) {
-                const int32_t s = b[j];
-                if (x == s) {                                   /* MP1Node.cpp:237-243 */
-                    if (present) { cur.hb += 1; cur.ts = t; }
-                    else { present = 1; cur.hb = 1; cur.ts = t; }
-                    continue;
-                }
-                const pv_ent *v = find_id(o->tab[prev] + (size_t)s * V, o->len[prev][s], x);
-                if (!v) continue;
-                if (present) {                                  /* MP1Node.cpp:247-251 */
-                    if (v->hb > cur.hb) { cur.hb = v->hb; cur.ts = t; }
-                } else if (x != r && t - v->ts < T) {           /* MP1Node.cpp:282-301 */
-                    present = 1; cur.hb = v->hb; cur.ts = v->ts;
-                }
-            }
-            if (!present) continue;
-            if (!e0) { d->joins++; d->event_hash += gsp_pv_event_mix(1, t, r, x); }
-            if (t - cur.ts >= T) {                              /* MP1Node.cpp:340 */
-                d->removes++; d->event_hash += gsp_pv_event_mix(2, t, r, x);
-                continue;
-            }
-            res[nres++] = cur;
-        }
+        const int32_t nres = pv_row_step(c, t, r, own, own_len, k, b, sv, slen, out, d, ids, res, kk);
         o->own_hb[r] += 1;
-        if (nres > V) {
-            for (int32_t i = 0; i < nres; ++i) { kk[i].e = res[i]; kk[i].age = t - res[i].ts; }
-            qsort(kk, nres, sizeof(keyed), cmp_keep);
-            for (int32_t i = V; i < nres; ++i) {
-                d->evicts++;
-                d->event_hash += gsp_pv_event_mix(3, t, r, kk[i].e.id);
-            }
-            for (int32_t i = 0; i < V; ++i) res[i] = kk[i].e;
-            nres = V;
-            qsort(res, nres, sizeof(pv_ent), cmp_id);
-        }
-        memcpy(out, res, sizeof(pv_ent) * nres);
         o->len[next][r] = nres;
     }
-    free(deg); free(fill); free(bucket); free(ids); free(res); free(kk);
+    free(deg); free(fill); free(bucket); free(ids); free(res); free(kk); free(sv); free(slen);
     o->cur = next;
     o->t = t;
     pv_send_all(o, next, t, d);

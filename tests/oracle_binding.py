@@ -68,6 +68,7 @@ def load_oracle():
         L.gsp_oracle_mp1_run.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
                                          ctypes.c_int] + [ctypes.c_char_p] * 4
         L.gsp_oracle_mp1_run.restype = ctypes.c_int
+        L.gsp_oracle_mp1_buffer_full_rejects.restype = ctypes.c_int64
         L.gsp_glibc_stream.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32),
                                        ctypes.c_int64]
         L.gsp_scale_oracle_create.argtypes = [ctypes.POINTER(ScaleCfg)]
@@ -97,6 +98,12 @@ def load_oracle():
         L.gsp_pview_oracle_messages.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_int64]
         L.gsp_pview_oracle_messages.restype = ctypes.c_int64
+        L.gsp_pview_oracle_row_step.argtypes = [ctypes.POINTER(PviewCfg), ctypes.c_int32,
+                                                ctypes.c_int32] + [ctypes.c_void_p] * 3 + [
+            ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 8 + [ctypes.POINTER(PviewDigest)]
+        L.gsp_pview_oracle_row_step.restype = ctypes.c_int32
+        L.gsp_oracle_draw.argtypes = [ctypes.c_uint32, ctypes.c_uint64] + [ctypes.c_uint32] * 4
+        L.gsp_oracle_draw.restype = ctypes.c_uint32
         _oracle = L
     return _oracle
 
@@ -107,7 +114,49 @@ def golden(mode, conf, seed, name):
 
 
 def conf_path(conf):
+    if conf in BIG_CONFS:
+        return os.path.join(GOLDEN_BIG, "testcases", conf + ".conf")
     return os.path.join(GOLDEN, "testcases", conf + ".conf")
+
+
+# Fixtures past the reference's N = 10 (tests/golden/make_golden.py --big): MAX_NNB 70 / 300 /
+# 600, made by the reference itself; state.txt is kept as per-tick SHA-256 + selected ticks.
+GOLDEN_BIG = os.path.join(ROOT, "tests", "golden", "ref_big")
+BIG_CONFS = ["n70_single", "n70_multi", "n70_drop", "n300_single", "n300_multi", "n300_drop",
+             "n600_multidrop", "n600_single"]
+BIG_RUNS = [(c, s, m) for c in BIG_CONFS if not c.startswith("n600") for s in (3, 77)
+            for m in MODES] + [(c, 3, m) for c in BIG_CONFS if c.startswith("n600") for m in MODES]
+BIG_FILES = ["dbg.log", "msgcount.log", "stdout.txt", "state_sha.txt", "state_sel.txt"]
+STATE_SEL = (99, 100, 101, 121, 299, 300, 699)
+
+
+def golden_big(mode, conf, seed, name):
+    with gzip.open(os.path.join(GOLDEN_BIG, mode, conf, str(seed), name + ".gz"), "rb") as f:
+        return f.read()
+
+
+def state_digest(state_bytes):
+    """(per-tick SHA-256 lines, lines of the STATE_SEL ticks) of a state dump -- the form the
+    big fixtures keep (same function as tests/golden/make_golden.py)."""
+    import hashlib
+    by_tick = {}
+    for line in state_bytes.splitlines(keepends=True):
+        by_tick.setdefault(int(line.split(b" ", 1)[0]), []).append(line)
+    sha = b"".join(b"%d %s\n" % (t, hashlib.sha256(b"".join(v)).hexdigest().encode())
+                   for t, v in sorted(by_tick.items()))
+    sel = b"".join(b"".join(by_tick.get(t, [])) for t in STATE_SEL)
+    return sha, sel
+
+
+def outputs_for_big(paths):
+    """The BIG_FILES view of a run's output files (dbg / msgcount / stdout / state)."""
+    out = {}
+    for name in ["dbg.log", "msgcount.log", "stdout.txt"]:
+        with open(paths[name], "rb") as f:
+            out[name] = f.read()
+    with open(paths["state.txt"], "rb") as f:
+        out["state_sha.txt"], out["state_sel.txt"] = state_digest(f.read())
+    return out
 
 
 def run_oracle_mp1(conf, seed, mode, out_dir, ticks=700):
@@ -166,6 +215,35 @@ class ScaleOracle:
 
     def __del__(self):
         self.close()
+
+
+def pview_row_step(cfg, t, r, own, senders, views):
+    """oracle/pview_oracle.c's per-row rule for one row (gsp_pview_oracle_row_step).
+    own / views[j]: (ids, hb, ts) with ascending ids and absolute ts; senders[j] sent views[j].
+    Returns ((ids, hb, ts) of r's new view, the row's digest counts)."""
+    import numpy as np
+    L = load_oracle()
+    V = cfg.view
+    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)
+    oi, oh, ot = (i32(x) for x in own)
+    k = len(senders)
+    sid = np.zeros((max(k, 1), V), np.int32)
+    shb = np.zeros_like(sid)
+    sts = np.zeros_like(sid)
+    slen = np.zeros(max(k, 1), np.int32)
+    for j, (vi, vh, vt) in enumerate(views):
+        m = len(vi)
+        sid[j, :m], shb[j, :m], sts[j, :m], slen[j] = vi, vh, vt, m
+    snd = i32(list(senders) or [0])
+    out = [np.zeros(V, np.int32) for _ in range(3)]
+    d = PviewDigest()
+    m = L.gsp_pview_oracle_row_step(ctypes.byref(cfg), t, r, oi.ctypes.data, oh.ctypes.data,
+                                    ot.ctypes.data, len(oi), k, snd.ctypes.data, sid.ctypes.data,
+                                    shb.ctypes.data, sts.ctypes.data, slen.ctypes.data,
+                                    out[0].ctypes.data, out[1].ctypes.data, out[2].ctypes.data,
+                                    ctypes.byref(d))
+    assert m >= 0
+    return tuple(x[:m] for x in out), d.as_dict()
 
 
 class PviewOracle:

@@ -43,6 +43,27 @@ def test_application_bitexact(tmp_path, conf, seed, mode):
     assert os.path.exists(os.path.join(str(tmp_path), "stats.log"))
 
 
+def test_grader_directory_90():
+    """grader/ is the layout Grader.sh drives unmodified: for each scenario it runs
+    `make clean; make; ./Application testcases/<x>.conf` in that directory
+    (/root/reference/Grader.sh:32-34, 81-83, 144-146) and greps dbg.log; tests/grader.py
+    restates the greps.  The same command sequence here must score 90/90."""
+    gdir = os.path.join(ROOT, "grader")
+    env = {k: v for k, v in os.environ.items() if k not in ("GSP_SEED", "GSP_RNG")}
+    total = 0
+    try:
+        for conf in CONFS:
+            r = subprocess.run(["bash", "-c", "make clean > /dev/null && make > /dev/null && "
+                                "./Application testcases/%s.conf > /dev/null" % conf],
+                               cwd=gdir, env=env, capture_output=True, timeout=300)
+            assert r.returncode == 0, r.stderr.decode()
+            with open(os.path.join(gdir, "dbg.log"), "rb") as f:
+                total += grader.score(f.read(), conf)
+    finally:
+        subprocess.run(["make", "clean"], cwd=gdir, capture_output=True)
+    assert total == 90
+
+
 def test_application_grader_90(tmp_path):
     total = 0
     env = {k: v for k, v in os.environ.items() if k not in ("GSP_SEED", "GSP_RNG")}

@@ -44,3 +44,25 @@ def test_exact_stale_payload_is_rejected():
         e.recv(2, [1])
         with pytest.raises(Exception, match="stale payload"):
             e.process(2, [1], [exact.OP_LOOP], 0)
+
+
+from tests.oracle_binding import BIG_FILES, BIG_RUNS, golden_big, outputs_for_big  # noqa: E402
+
+
+@pytest.mark.parametrize("conf,seed,mode", BIG_RUNS, ids=lambda x: str(x))
+def test_exact_bitexact_vs_reference_big(tmp_path, conf, seed, mode):
+    """Past the reference's N = 10 testcases: MAX_NNB 70 / 300 / 600 against the reference's
+    own outputs (tests/golden/ref_big).  Covers msgcount.log's node-67 layout
+    (EmulNet.cpp:204-211), negative address bytes of ids >= 128 (Log.cpp:73), strcmp()
+    delivery aliasing of ids 256 / 512 (EmulNet.cpp:154), the full 30,000-message buffer
+    (EmulNet.cpp:92) and the id < 10 payload filter at N > 10 (MP1Node.cpp:245)."""
+    got = outputs_for_big(exact.run_application(conf_path(conf), seed, mode, str(tmp_path)))
+    for name in BIG_FILES:
+        want = golden_big(mode, conf, seed, name)
+        if got[name] != want:
+            gl, wl = got[name].decode().splitlines(), want.decode().splitlines()
+            first = next((i for i, (a, b) in enumerate(zip(gl, wl)) if a != b),
+                         min(len(gl), len(wl)))
+            pytest.fail("%s differs at line %d:\n got: %s\nwant: %s" % (
+                name, first, gl[first][:300] if first < len(gl) else "<eof>",
+                wl[first][:300] if first < len(wl) else "<eof>"))

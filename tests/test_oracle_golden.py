@@ -79,3 +79,46 @@ def test_golden_state_shape():
     st = golden("glibc", "singlefailure", 10, "state.txt").decode().splitlines()
     assert len(st) == 700 * 10
     assert re.match(r"^0 1 1 1 0 0 0$", st[0])
+
+
+# ---- past N = 10: the reference's own outputs at MAX_NNB 70 / 300 / 600 -------------------
+from tests.oracle_binding import (BIG_FILES, BIG_RUNS, golden_big, outputs_for_big)  # noqa: E402
+
+
+@pytest.mark.parametrize("conf,seed,mode", BIG_RUNS, ids=lambda x: str(x))
+def test_oracle_matches_reference_big(tmp_path, conf, seed, mode):
+    """The C restatement reproduces the reference at N = 70 / 300 / 600: dbg.log,
+    msgcount.log, stdout byte for byte and the end-of-tick state of every node at every tick
+    (per-tick SHA-256, full lines at selected ticks)."""
+    got = outputs_for_big(run_oracle_mp1(conf, seed, mode, str(tmp_path)))
+    for name in BIG_FILES:
+        assert got[name] == golden_big(mode, conf, seed, name), "%s %s %s %s" % (
+            conf, seed, mode, name)
+
+
+def test_big_fixtures_reach_the_reference_quirks(tmp_path):
+    """The large-N fixtures exercise what N = 10 never does (each a reference behaviour the
+    parity tests would otherwise leave unpinned)."""
+    # msgcount.log's node-67 layout (EmulNet.cpp:204-211)
+    mc = golden_big("glibc", "n70_multi", 3, "msgcount.log").decode()
+    assert "node  67 special    0" in mc and "node  67 sent_total" in mc
+    # signed-char address bytes of ids >= 128 (Log.cpp:73): id 128 prints as -128.0.0.0
+    assert b" -128.0.0.0:0 [0] APP" in golden_big("glibc", "n300_single", 3, "dbg.log")
+    # strcmp() address aliasing (EmulNet.cpp:154): ids 256, 512 (first byte 0) share one
+    # class, so node 256 -- which receives first (ascending order) -- also takes the messages
+    # sent to 512; node 512 receives nothing in a whole run although it is sent to
+    lines = golden_big("glibc", "n600_single", 3, "msgcount.log").decode().splitlines()
+    tot = {int(l.split()[1]): (int(l.split()[3]), int(l.split()[5]))
+           for l in lines if "sent_total" in l}
+    assert tot[512][1] == 0 and tot[256][1] > tot[255][1]
+    # the 30,000-message EmulNet buffer fills (EmulNet.cpp:92): messages to the multi-failure
+    # victims linger; the oracle counts the sends it rejected for that reason
+    L = load_oracle()
+    run_oracle_mp1("n600_multidrop", 3, "glibc", str(tmp_path))
+    assert L.gsp_oracle_mp1_buffer_full_rejects() > 0
+    run_oracle_mp1("n70_multi", 3, "glibc", str(tmp_path))
+    assert L.gsp_oracle_mp1_buffer_full_rejects() == 0
+    # the id < 10 payload filter (MP1Node.cpp:245) at N > 10: only ids 1..9 spread
+    # indirectly, so far fewer join lines than the N (N - 1) of a full view
+    joins = golden_big("glibc", "n300_single", 3, "dbg.log").count(b"joined")
+    assert joins < 300 * 299 // 4

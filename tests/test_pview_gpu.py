@@ -134,3 +134,90 @@ def test_pview_rccl_one_rank():
             assert a.digest(t) == b.digest(t)
         for r in range(0, n, 37):
             assert a.row(r)[1] == b.row(r)[1] and np.array_equal(a.row(r)[0], b.row(r)[0])
+
+
+def test_pview_capacity_error_stops_the_job(monkeypatch):
+    """A receiver sent more messages than the receipt bound (1,024; lowered to 2 through the
+    test-only GSP_TEST_MAX_SEGMENT) stops the job at that tick: its tick kernel and every later
+    one run no row, and the next step call and every read return GSP_ERR_CAPACITY."""
+    from gossip_protocol_amd._lib import GspError
+    monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
+    with PviewEngine(300, view=64, fanout=8, inbox=7, max_ticks=10) as eng:
+        eng.step(1)
+        with pytest.raises(GspError, match="more than 2 messages at tick 1"):
+            eng.step(1)
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.digest(1)
+    monkeypatch.delenv("GSP_TEST_MAX_SEGMENT")
+    with PviewEngine(300, view=64, fanout=8, inbox=7, max_ticks=10) as eng:
+        eng.step(3)
+        assert eng.digest(3)["node_rounds"] == 300
+
+
+def test_pview_full_size_properties():
+    """BASELINE config 5 at its real size on one GPU: 1,048,576 nodes, V = 256, fanout 3,
+    inbox 7, 10 % drop, 5 % contiguous crash at t = 10 -- the bench's line item, checked.
+
+    * node-rounds = the alive count (every node up to tick 10, n - 52,428 after);
+    * the message list of tick 12 is the digest's sent - dropped, crashed nodes send nothing,
+      and tick 13 delivers or overflows exactly the messages addressed to alive nodes;
+    * sampled views are sorted, distinct, never list their owner and hold <= V entries;
+    * rows of tick 13 recomputed on the host from the tick-12 views and the message list by
+      oracle/pview_oracle.c's per-row rule (gsp_pview_oracle_row_step: the reference's merge /
+      TREMOVE rules, MP1Node.cpp:234-301, 339-348, plus the bounded view's eviction) equal the
+      device's -- for receivers with 0, 1, 3 and more than 7 (inbox overflow) messages, which
+      exercises the 21-bit id field, every view-count variant class and eviction at full load.
+    """
+    from tests.oracle_binding import PviewCfg, load_oracle, pview_row_step
+    n, seed, ftick, ppm = 1 << 20, 0x5EED, 10, 50000
+    kw = dict(view=256, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=ftick,
+              fail_ppm=ppm, seed=seed)
+    cfg = PviewCfg(n, 256, 3, 7, 10, 20, 1, 2, ftick, ppm, seed)
+    # the crashed block, from the oracle's Philox (oracle/pview_oracle.c pv_fail_ticks)
+    start = load_oracle().gsp_oracle_draw(0x4641494C, seed, ftick, 0xFFFFFFFF, 0, 0) % n
+    m = n * ppm // 1000000
+    dead = np.zeros(n, bool)
+    dead[(start + np.arange(m)) % n] = True
+    with PviewEngine(n, max_ticks=16, **kw) as eng:
+        eng.step(12)
+        ds = {t: eng.digest(t) for t in range(1, 13)}
+        for t in range(1, 13):
+            assert ds[t]["node_rounds"] == (n if t <= ftick else n - m), t
+            assert ds[t]["delivered"] <= 7 * ds[t]["node_rounds"]
+        msgs = eng.messages()                       # sent at tick 12, merged at 13
+        assert msgs.shape == (n, 3)
+        assert (msgs[dead] < 0).all()
+        live = msgs[msgs >= 0]
+        assert len(live) == ds[12]["sent"] - ds[12]["dropped"]
+        cnt = np.bincount(live, minlength=n)
+        rng = np.random.default_rng(5)
+        alive_rows = np.nonzero(~dead)[0]
+        targets = []
+        for want in (0, 1, 3):
+            cand = alive_rows[cnt[alive_rows] == want]
+            targets.append(int(cand[rng.integers(len(cand))]))
+        cand = alive_rows[cnt[alive_rows] > 7]
+        assert len(cand) > 0
+        targets.append(int(cand[rng.integers(len(cand))]))
+        targets.append(int(alive_rows[np.argmax(cnt[alive_rows])]))
+        senders = {r: np.nonzero((msgs == r).any(axis=1))[0].tolist() for r in targets}
+
+        def view(x, t):                             # (ids, hb, absolute ts) of x at tick t
+            buf, ln = eng.row(x)
+            ids, hb, ts5 = unpack_view(buf, ln)
+            assert ln <= 256 and np.all(np.diff(ids) > 0) and x not in ids
+            return ids, hb, t - ((t - ts5) & 31)
+
+        prev = {x: view(x, 12) for x in set(targets) | {s for v in senders.values() for s in v}}
+        for x in rng.integers(0, n, 64).tolist():
+            view(x, 12)
+        eng.step(1)
+        d13 = eng.digest(13)
+        assert d13["delivered"] + d13["overflow"] == int(cnt[~dead].sum())
+        for r in targets:
+            (ids, hb, ts), _ = pview_row_step(cfg, 13, r, prev[r], senders[r],
+                                              [prev[s] for s in senders[r]])
+            gi, gh, gt = view(r, 13)
+            assert np.array_equal(gi, ids), "ids of row %d (%d senders)" % (r, len(senders[r]))
+            assert np.array_equal(gh, hb), "hb of row %d" % r
+            assert np.array_equal(gt, ts), "ts of row %d" % r

@@ -301,3 +301,23 @@ def test_scale_full_size_properties():
             e[r] = 0
             e = np.where((e != 0) & (((t5 - e) & 31) >= tr), 0, e)
             assert np.array_equal(e.astype(np.uint16), eng.row(r)), "row %d" % r
+
+
+def test_capacity_error_stops_the_job(monkeypatch):
+    """A receiver sent more messages than the kernel's segment bound (1,024; lowered to 2 here
+    through the test-only GSP_TEST_MAX_SEGMENT) stops the job loudly: the device flags the
+    tick, every later tick kernel runs no row, and the next gsp_scale_step call (no host
+    synchronisation needed) and every read return GSP_ERR_CAPACITY instead of state computed
+    from a skipped row."""
+    from gossip_protocol_amd._lib import GspError
+    monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
+    with ScaleEngine(256, fanout=8, max_ticks=10) as eng:
+        eng.step(1)                      # tick 1: ~8 messages per receiver > 2
+        with pytest.raises(GspError, match="more than 2 messages at tick 1"):
+            eng.step(1)
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.digest(1)
+    monkeypatch.delenv("GSP_TEST_MAX_SEGMENT")
+    with ScaleEngine(256, fanout=8, max_ticks=10) as eng:   # the default bound: no error
+        eng.step(3)
+        assert eng.digest(3)["node_rounds"] == 256
