@@ -38,6 +38,83 @@ FAIL_TICK = 10
 SEED = 0x5EED
 
 
+def host_cpu():
+    """CPU model and core counts of this host (the CPU baseline runs on one of them)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_usable": usable}
+
+
+REF_APP = os.path.join(ROOT, "oracle", "_ref", "Application")
+REF_CONFS = {"singlefailure": (1, 0), "multifailure": (0, 0), "msgdropsinglefailure": (1, 1)}
+
+
+def ref_node_rounds(dbg, n=10, ticks=700):
+    """nodeLoop calls of one reference run (Application.cpp:153-155): node i runs at tick t iff
+    t > 0.25 i (double compare) and it has not failed; the failed nodes (Application::fail at
+    t = 100, Application.cpp:173-202) are read back from the run's dbg.log lines."""
+    failed = set()
+    for line in dbg.decode(errors="replace").split("\n"):
+        if "Node failed at time" in line:
+            failed.add(int(line.split()[0].split(".")[0]) & 0xFF)
+    rounds = 0
+    for i in range(n):
+        active = sum(1 for t in range(ticks) if t > 0.25 * i)
+        rounds += active - (ticks - 1 - 100 if (i + 1) in failed else 0)
+    return rounds
+
+
+def reference_cpu_baseline(budget_s=8.0):
+    """The REFERENCE itself as the CPU baseline: oracle/_ref/Application -- the unmodified
+    /root/reference sources built by oracle/Makefile with the reference's own flags (-g, i.e.
+    -O0, Makefile:10) plus a time() pin for the seed -- run single-threaded on this host over
+    its three testcases (N = 10, 700 ticks, Application.cpp:90-114) for ~budget_s seconds.
+    node-rounds/s = nodeLoop calls / whole-process wall time (constructor and msgcount.log
+    included; the reference cannot run the GPU configs: MAX_NODES = 1000, EmulNet.h:10)."""
+    import shutil
+    import subprocess
+    import tempfile
+    if not os.path.exists(REF_APP):
+        return None
+    src = os.path.join(ROOT, "tests", "golden", "ref", "testcases")
+    rounds = runs = 0
+    wall = 0.0
+    with tempfile.TemporaryDirectory() as tmp:
+        os.makedirs(os.path.join(tmp, "testcases"))
+        for c in REF_CONFS:
+            shutil.copy(os.path.join(src, c + ".conf"), os.path.join(tmp, "testcases"))
+        seed = 1
+        t_end = time.perf_counter() + budget_s
+        while time.perf_counter() < t_end:
+            for c in REF_CONFS:
+                env = dict(os.environ, GSP_SEED=str(seed))
+                a = time.perf_counter()
+                subprocess.run([REF_APP, "testcases/%s.conf" % c], cwd=tmp, env=env, check=True,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+                wall += time.perf_counter() - a
+                with open(os.path.join(tmp, "dbg.log"), "rb") as f:
+                    rounds += ref_node_rounds(f.read())
+                runs += 1
+            seed += 1
+    out = {"value": rounds / wall, "unit": "node-rounds/s", "cores": 1, "kind": "reference",
+           "sample": "oracle/_ref/Application (the reference, -O0 as its Makefile builds it), "
+                     "%d runs of its 3 testcases (N = 10, 700 ticks, seeds 1..%d), %d node-rounds "
+                     "in %.2f s of whole-process wall time, 1 thread" % (runs, seed - 1, rounds, wall)}
+    out.update(host_cpu())
+    return out
+
+
 def cpu_baseline(budget_s=12.0):
     """Oracle restatement (oracle/scale_oracle.c, 1 thread) on a bounded sample.
 
@@ -326,7 +403,13 @@ def main(argv=None):
         out.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                     "higher_is_better": True, "vs_baseline": None})
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline()
+            # the reference itself (N = 10, the only size it runs), with our restatement of
+            # the config-3 protocol beside it (scaled to 65,536-wide rows)
+            port = cpu_baseline()
+            ref = reference_cpu_baseline()
+            out["cpu_baseline"] = ref if ref is not None else port
+            if ref is not None:
+                out["cpu_baseline"]["port"] = port
 
     # Secondary line items: an exception is recorded in the item (every rank sees the same
     # deterministic capacity / allocation errors); a hang or a one-rank failure that stalls
