@@ -79,6 +79,20 @@ int32_t gsp_scale_oracle_fail_tick(const gsp_scale_oracle *o, int32_t r);
 int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32_t *dst,
                                   int64_t cap);
 
+/* The scale protocol's per-row rules (the reference's, MP1Node.cpp:237-251, 282-301, 339-348),
+ * exported so tests can feed them the reference's own rows: one GOSSIP merge, and the
+ * TREMOVE scan (returns the gossipable member count). */
+void gsp_scale_oracle_merge_msg(int32_t n, int32_t t, int32_t T, int32_t tfail, int32_t r,
+                                uint8_t *P, int32_t *H, int32_t *S, int32_t s, const uint8_t *Ps,
+                                const int32_t *Hs, const int32_t *Ss, int64_t *joins,
+                                uint64_t *hash);
+int32_t gsp_scale_oracle_remove_scan(int32_t n, int32_t t, int32_t T, int32_t tfail, int32_t r,
+                                     uint8_t *P, int32_t *H, int32_t *S, int64_t *removes,
+                                     uint64_t *hash);
+/* mp1 restatement: the next gsp_oracle_mp1_run writes every message a node handles, in
+ * handling order, to `path` (NULL: off) as "t receiver_id src_id type send_tick" lines. */
+void gsp_oracle_mp1_set_queue_trace(const char *path);
+
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x);
 uint64_t gsp_pv_event_mix(int kind, int64_t t, int64_t r, int64_t x);   /* partial view */
 

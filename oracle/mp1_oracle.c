@@ -30,6 +30,7 @@ typedef struct {
     entry_t *payload; /* GOSSIP: copy of the sender's list at send time (MP1Node.cpp:357) */
     int npayload;
     int dkey;         /* addr_key(dst): the destination address as strcmp() sees it */
+    int st;           /* send tick */
 } msg_t;
 
 typedef struct {
@@ -118,6 +119,13 @@ static int addr_key(int id) {
 /* sends the last gsp_oracle_mp1_run rejected because the 30,000-message buffer was full
  * (EmulNet.cpp:92): lets the fixture tests show that a case reaches that path */
 static int64_t g_buffer_full_rejects;
+/* optional handling-order trace (gsp_oracle_mp1_set_queue_trace) */
+static char g_trace_path[4096];
+static FILE *g_trace;
+void gsp_oracle_mp1_set_queue_trace(const char *path) {
+    g_trace_path[0] = 0;
+    if (path) snprintf(g_trace_path, sizeof g_trace_path, "%s", path);
+}
 int64_t gsp_oracle_mp1_buffer_full_rejects(void) { return g_buffer_full_rejects; }
 
 /* ---------------- EmulNet (EmulNet.cpp) ---------------- */
@@ -127,7 +135,7 @@ static void en_send(sim_t *s, int src_node, int dst_id, int type, const entry_t 
     int thr = (int)(s->drop_prob * 100);                   /* EmulNet.cpp:91               */
     if (s->nbuf >= EN_BUFF_CAP) { g_buffer_full_rejects++; return; }   /* EmulNet.cpp:92 */
     if (s->dropmsg && r % 100 < thr) return;
-    msg_t m = {src_node + 1, dst_id, type, NULL, 0, addr_key(dst_id)};
+    msg_t m = {src_node + 1, dst_id, type, NULL, 0, addr_key(dst_id), s->t};
     if (type == M_GOSSIP && npl) {
         m.payload = malloc(sizeof(entry_t) * npl);
         memcpy(m.payload, pl, sizeof(entry_t) * npl);
@@ -233,7 +241,12 @@ static void node_start(sim_t *s, int node) {             /* MP1Node.cpp:67-154 *
 static void node_loop(sim_t *s, int node) {              /* MP1Node.cpp:176-212 */
     node_t *nd = &s->nodes[node];
     if (nd->failed) return;
-    for (int i = 0; i < nd->nqueue; ++i) handle(s, node, &nd->queue[i]);
+    for (int i = 0; i < nd->nqueue; ++i) {
+        if (g_trace)
+            fprintf(g_trace, "%d %d %d %d %d\n", s->t, node + 1, nd->queue[i].src,
+                    nd->queue[i].type, nd->queue[i].st);
+        handle(s, node, &nd->queue[i]);
+    }
     nd->nqueue = 0;
     if (!nd->in_group) return;
     node_ops(s, node);
@@ -312,6 +325,7 @@ int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int t
     sim_t s;
     memset(&s, 0, sizeof s);
     g_buffer_full_rejects = 0;
+    g_trace = g_trace_path[0] ? fopen(g_trace_path, "w") : NULL;
     if (read_conf(&s, conf_path) != 0) return -1;
     if (s.n <= 0 || s.n > 1000 || ticks <= 0 || ticks > MAX_TICKS) return -2;
     s.rng_mode = rng_mode;
@@ -352,6 +366,7 @@ int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int t
     if (msgcount_path) write_msgcount(&s, msgcount_path);
 
     if (s.dbg) fclose(s.dbg);
+    if (g_trace) { fclose(g_trace); g_trace = NULL; }
     if (st) fclose(st);
     if (out) fclose(out);
     for (int k = 0; k < s.nbuf; ++k) free(s.buf[k].payload);

@@ -136,6 +136,54 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
     }
 }
 
+/* ---- the per-row rules, exported (tests/test_scale_rules_vs_reference.py feeds them the
+ * reference's own rows and message order) ---- */
+
+/* Receiver row r merges ONE GOSSIP sent by s at tick t - 1, at tick t.  P/H/S: r's row
+ * (presence, hb, absolute ts) over n columns; Ps/Hs/Ss: s's row as s sent it.
+ *   sender entry:  present -> hb += 1, ts = t; absent -> add (1, t)     MP1Node.cpp:237-243
+ *   payload entry: present -> if v.hb > hb: hb = v.hb, ts = t           MP1Node.cpp:247-251
+ *                  absent  -> add a copy of v if v.id != r, t - v.ts < T MP1Node.cpp:282-301
+ * With tfail > 0 the payload holds only what s could gossip at t - 1.  Join events are
+ * counted into *joins and hashed into *hash. */
+void gsp_scale_oracle_merge_msg(int32_t n, int32_t t, int32_t T, int32_t tfail, int32_t r,
+                                uint8_t *P, int32_t *H, int32_t *S, int32_t s, const uint8_t *Ps,
+                                const int32_t *Hs, const int32_t *Ss, int64_t *joins,
+                                uint64_t *hash) {
+    if (P[s]) { H[s] += 1; S[s] = t; }
+    else {
+        P[s] = 1; H[s] = 1; S[s] = t;
+        (*joins)++; *hash += gsp_event_mix(1, t, r, s);
+    }
+    for (int32_t x = 0; x < n; ++x) {
+        if (!Ps[x] || x == s || !(tfail <= 0 || (t - 1) - Ss[x] < tfail)) continue;
+        if (P[x]) {
+            if (Hs[x] > H[x]) { H[x] = Hs[x]; S[x] = t; }
+        } else if (x != r && t - Ss[x] < T) {
+            P[x] = 1; H[x] = Hs[x]; S[x] = Ss[x];
+            (*joins)++; *hash += gsp_event_mix(1, t, r, x);
+        }
+    }
+}
+
+/* nodeLoopOps' TREMOVE scan of row r at tick t (MP1Node.cpp:339-348): entries with
+ * t - ts >= T are removed (events counted / hashed); returns the gossipable member count. */
+int32_t gsp_scale_oracle_remove_scan(int32_t n, int32_t t, int32_t T, int32_t tfail, int32_t r,
+                                     uint8_t *P, int32_t *H, int32_t *S, int64_t *removes,
+                                     uint64_t *hash) {
+    int32_t live = 0;
+    for (int32_t x = 0; x < n; ++x) {
+        if (!P[x]) continue;
+        if (t - S[x] >= T) {
+            P[x] = 0; H[x] = 0; S[x] = 0;
+            (*removes)++; *hash += gsp_event_mix(2, t, r, x);
+        } else {
+            live += tfail <= 0 || t - S[x] < tfail;
+        }
+    }
+    return live;
+}
+
 gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg) {
     if (!cfg || cfg->n < 2 || cfg->fanout < 1 || cfg->fanout > 60 ||
         cfg->swim < 0 || cfg->swim > 8) return NULL;
@@ -223,21 +271,9 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
             const int32_t *Hs = o->hb[prev] + srow, *Ss = o->ts[prev] + srow;
             d->delivered++;
             d->merges += 1 + o->cnt[s];
-            if (P[s]) { H[s] += 1; S[s] = t; }
-            else {
-                P[s] = 1; H[s] = 1; S[s] = t;
-                d->joins++; d->event_hash += gsp_event_mix(1, t, r, s);
-            }
-            for (int32_t x = 0; x < n; ++x) {
-                /* the payload: s's members gossipable when s sent it (tick t - 1) */
-                if (!Ps[x] || x == s || !gossipable(c, t - 1, Ss[x])) continue;
-                if (P[x]) {
-                    if (Hs[x] > H[x]) { H[x] = Hs[x]; S[x] = t; }
-                } else if (x != r && t - Ss[x] < T) {
-                    P[x] = 1; H[x] = Hs[x]; S[x] = Ss[x];
-                    d->joins++; d->event_hash += gsp_event_mix(1, t, r, x);
-                }
-            }
+            /* the payload: s's members gossipable when s sent it (tick t - 1) */
+            gsp_scale_oracle_merge_msg(n, t, T, c->tfail, r, P, H, S, s, Ps, Hs, Ss, &d->joins,
+                                       &d->event_hash);
         }
         if (c->swim > 0 && o->ping[r] >= 0) {   /* resolve the probe sent at t - 1 */
             const int32_t p = o->ping[r];
@@ -248,17 +284,8 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
             if (P[p]) S[p] = (ok && alive_at(o, p, t)) ? t : t - T;
         }
         o->own_hb[r] += 1;
-        int32_t live = 0;
-        for (int32_t x = 0; x < n; ++x) {
-            if (!P[x]) continue;
-            if (t - S[x] >= T) {
-                P[x] = 0; H[x] = 0; S[x] = 0;
-                d->removes++; d->event_hash += gsp_event_mix(2, t, r, x);
-            } else {
-                live += gossipable(c, t, S[x]);
-            }
-        }
-        cnt_next[r] = live;
+        cnt_next[r] = gsp_scale_oracle_remove_scan(n, t, T, c->tfail, r, P, H, S, &d->removes,
+                                                   &d->event_hash);
     }
     memcpy(o->cnt, cnt_next, sizeof(int32_t) * n);
     free(cnt_next); free(deg); free(fill); free(bucket);
