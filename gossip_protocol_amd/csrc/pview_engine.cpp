@@ -39,14 +39,14 @@ struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
-        tile_sum, rc_info, rc_src, rc_slot;
+        tile_sum, rc_info, rc_src, rc_slot, kcount, order;
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     gsp::RowxBufs x;             // row exchange (G > 1)
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
         for (auto *b : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &err,
-                        &tile_sum, &rc_info, &rc_src, &rc_slot})
+                        &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order})
             b->release();
         x.release();
         dig.release();
@@ -70,6 +70,7 @@ struct gsp_pview {
     bool timing = true;
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
     int32_t max_segment = gsp::kPvMaxSegment;
+    bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail;
@@ -119,6 +120,8 @@ struct gsp_pview {
         a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
         a.err = sh.err.p;
         a.max_segment = max_segment;
+        a.kcount = sort_rows ? sh.kcount.p : nullptr;
+        a.order = sort_rows ? sh.order.p : nullptr;
         a.prof = sh.prof.p;
         a.waves = waves;
         return a;
@@ -137,6 +140,8 @@ struct gsp_pview {
         a.rc_info = sh.rc_info.p;
         a.rc_src = sh.rc_src.p;
         a.rc_slot = sh.rc_slot.p;
+        a.kcount = sort_rows ? sh.kcount.p : nullptr;
+        a.order = sort_rows ? sh.order.p : nullptr;
         a.err = sh.err.p;
         return a;
     }
@@ -191,6 +196,10 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     GSP_HIP(sh.rc_src.alloc(rows * 8));
     GSP_HIP(sh.rc_slot.alloc(rows * 8));
     GSP_HIP(sh.rowdig.alloc(rows * 16));
+    if (s->sort_rows) {
+        GSP_HIP(sh.kcount.alloc(8));
+        GSP_HIP(sh.order.alloc(rows * 8));
+    }
     GSP_HIP(hipMemsetAsync(sh.rowdig.p, 0, rows * 16 * 8, st));
     if (s->rowmode)
         GSP_HIP(sh.x.alloc(G, s->pair_cap, s->msg_cap, V, int64_t(n) * F, st));
@@ -269,6 +278,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
+    if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
     gsp_scale_params fp{};
     fp.n = p->n; fp.fail_mode = p->fail_mode; fp.fail_tick = p->fail_tick;
     fp.fail_ppm = p->fail_ppm; fp.seed = p->seed;
@@ -394,7 +404,10 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
                                         sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
             GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
         }
-        for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
+        for (PvShard &sh : s->local) {
+            if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
+            GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
+        }
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));
         if (s->timing) {

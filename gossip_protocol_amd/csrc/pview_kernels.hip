@@ -188,12 +188,11 @@ struct RowOut {
 
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
-template <int kBlocks>
+template <int kBlocks, int kPre, typename Mid>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
-                                             int32_t k, uint64_t ent0,
-                                             const uint32_t (&ssrc)[kPvMaxInbox],
-                                             const int32_t (&sslot)[kPvMaxInbox], RowOut &ro,
-                                             PvMark &pm) {
+                                             int32_t k, const uint64_t (&pre)[kPre],
+                                             int32_t my_slot, const uint32_t (&ssrc)[kPvMaxInbox],
+                                             RowOut &ro, PvMark &pm, Mid &&mid) {
     constexpr int Q = kBlocks;                           // keys per lane
     constexpr int kJ = kBlocks - 1;                      // k <= kJ messages in this variant
     constexpr int P = kBlocks * kSlots;
@@ -205,15 +204,21 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     const uint64_t S_join = pv_seed(1, t, uint32_t(r)), S_remove = pv_seed(2, t, uint32_t(r)),
                    S_evict = pv_seed(3, t, uint32_t(r));
 
-    // ---- 2. keys: one sorted block of 256 slots per source -----------------------------------
+    // ---- 2. keys: one sorted block of 256 slots per source ------------------------------------
+    // entries [0, kPre) arrived with the row (the own view slot), the sender views are
+    // requested here (one coalesced 2 KB view each)
     uint64_t ent[kBlocks];
-    ent[0] = ent0;
 #pragma unroll
-    for (int m = 1; m < kBlocks; ++m) {
+    for (int m = 0; m < kBlocks; ++m) {
+        if (m < kPre) { ent[m] = pre[m < kPre ? m : 0]; continue; }
         ent[m] = kPvEmpty;
         if (m <= k && tid < V) {
-            const int32_t sl = sslot[m - 1];
+            const int32_t sl = __builtin_amdgcn_readlane(my_slot, m - 1);
+#ifdef GSP_PV_EXP_L2   // timing experiment only (wrong results): sender views from 64 hot rows
+            const uint64_t *row = a.prev + int64_t(sl & 63) * V;
+#else
             const uint64_t *row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
+#endif
             ent[m] = __builtin_nontemporal_load(row + tid);
         }
     }
@@ -228,13 +233,14 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
     }
     __syncthreads();
+    mid();                    // the next row's sender-view loads go out here (pipelined kernel)
     pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
     // Level s merges neighbouring segments of s keys (the last one of a level may be shorter
     // or alone when kBlocks is not a power of two).  The tree hands out Qt = 2^ceil(log2 Q)
     // outputs per lane, so a lane's outputs never straddle two merges (P / Qt lanes work).
-    constexpr int Qt = Q <= 2 ? Q : Q <= 4 ? 4 : 8;
+    constexpr int Qt = Q <= 2 ? Q : Q <= 4 ? 4 : 8;   // 8 or 16 for Q <= 4: +1 % / +6 %
     constexpr bool kPow2 = (kBlocks & (kBlocks - 1)) == 0;
     const int32_t begt = tid * Qt;
     int cur = 0;
@@ -586,121 +592,172 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
     }
 }
 
-// kWaves: minimum waves per SIMD the register allocation must allow (8 = 8 rows per CU, the
-// LDS limit; 7 = the allocator's own choice).  A/B switch: GSP_PV_WAVES.
-template <bool kInit, int kWaves>
-__global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
-    __shared__ PvShared sh;
+// What a row needs before its merge starts: the receipt record and its first kPre entries
+// (the own view slot); the sender views are loaded by the merge.
+template <int kPre>
+struct RowIn {
+    int32_t lr, info, my_src, my_slot;
+    uint64_t ent[kPre];
+};
+
+// workgroup-order index b -> row: b itself, or the b-th row of the k-descending order
+__device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) {
+    if (!a.order) return b;
+    int32_t q = 7;
+    for (; q > 0; --q) {
+        const int32_t c = a.kcount[q];
+        if (b < c) break;
+        b -= c;
+    }
+    return a.order[int64_t(q) * a.rows + b];
+}
+
+// stage 1: the own view slot and the receipt record (independent loads)
+template <int kPre>
+__device__ __forceinline__ void pv_load1(const PviewTickArgs &a, int32_t lr, RowIn<kPre> &in) {
     const int32_t tid = threadIdx.x, lane = tid & 63;
-    const int32_t lr = blockIdx.x;
-    const int32_t r = a.row0 + lr;
-    const int32_t V = a.view;
+    in.lr = lr;
+    in.ent[0] = tid < a.view ? __builtin_nontemporal_load(a.prev + int64_t(lr) * a.view + tid) : kPvEmpty;
+    in.info = a.rc_info[lr];
+    in.my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
+    in.my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
+}
 
-    // the own view is requested before anything else (its latency overlaps the record's)
-    const uint64_t ent0 = (!kInit && tid < V) ? __builtin_nontemporal_load(a.prev + int64_t(lr) * V + tid)
-                                              : kPvEmpty;
-    // the receipt record (pview_receipt_kernel) is requested next, before the liveness test,
-    // so the three loads' latencies overlap
-    int32_t info = 0, my_src = 0, my_slot = 0;
-    if constexpr (!kInit) {
-        info = a.rc_info[lr];
-        my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
-        my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
+// One non-init row from its record: merge, ops, eviction, view write, digest record.
+// mid() runs once on every path (after the key build, or at once for a row that does not run).
+template <int kPre, typename Mid>
+__device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, const RowIn<kPre> &in,
+                                       Mid &&mid) {
+    const int32_t tid = threadIdx.x;
+    const int32_t lr = in.lr, r = a.row0 + lr;
+    if (a.tick > a.fail_tick[r] || *a.err) {   // crashed (no recv, no ops, no send), or a
+        mid();                                 // capacity error stopped the job
+        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
+        return;
     }
-    if (a.tick > a.fail_tick[r] || (!kInit && *a.err)) {   // crashed (no recv, no ops, no
-        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;  // send), or a capacity error
-        return;                                                 // stopped the job
-    }
-
     PvMark pm;
     pm.init(a.prof);
     RowOut ro{};
-    int32_t k = 0, k_all = 0;
-    if (kInit) {
-        // pre-joined bounded view: {(r + 1 + j * (n / V)) mod n}, or everyone if n - 1 <= V
-        const int32_t n = a.n;
-        uint32_t *ids = sh.keys[0];
-        if (n - 1 <= V) {
-            for (int32_t x = tid; x < n; x += kPvBlock)
-                if (x != r) ids[x < r ? x : x - 1] = uint32_t(x);
-            ro.len = n - 1;
-        } else {
-            const int64_t stride = n / V;
-            const int64_t first_wrap = (int64_t(n) - r - 1 + stride - 1) / stride;
-            const int32_t J = int32_t(first_wrap < V ? first_wrap : V);
-            for (int32_t j = tid; j < V; j += kPvBlock) {
-                int64_t x = int64_t(r) + 1 + int64_t(j) * stride;
-                int32_t p;
-                if (x >= n) { x -= n; p = j - J; } else { p = j + (V - J); }
-                ids[p] = uint32_t(x);
-            }
-            ro.len = V;
-        }
-        for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
-        ro.ids_off = 0;
-        ro.vals_off = lds_half(sh, sh.vals);
-        __syncthreads();
-    } else {
-        // ---- 1. receipt record (loaded above), read by every wave -----------------------------
-        k = info & 7;
-        k_all = info >> 3;
-        uint32_t ssrc[kPvMaxInbox];
-        int32_t sslot[kPvMaxInbox];
+    const int32_t info = __builtin_amdgcn_readfirstlane(in.info);
+    const int32_t k = info & 7, k_all = info >> 3;
+    uint32_t ssrc[kPvMaxInbox];
 #pragma unroll
-        for (int jj = 0; jj < kPvMaxInbox; ++jj) {
-            ssrc[jj] = jj < k ? uint32_t(__builtin_amdgcn_readlane(my_src, jj)) : kNoId;
-            sslot[jj] = __builtin_amdgcn_readlane(my_slot, jj);
-        }
-        pm.mark(0);
-        // one variant per key count (own view + k sender views)
-        if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 2) pv_merge_row<3>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 3) pv_merge_row<4>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 4) pv_merge_row<5>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 5) pv_merge_row<6>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else if (k == 6) pv_merge_row<7>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        else pv_merge_row<8>(a, sh, r, k, ent0, ssrc, sslot, ro, pm);
-        pm.mark(5);
-    }
-    pv_finish(a, sh, lr, k, k_all, kInit, ro);
+    for (int jj = 0; jj < kPvMaxInbox; ++jj)
+        ssrc[jj] = jj < k ? uint32_t(__builtin_amdgcn_readlane(in.my_src, jj)) : kNoId;
+    pm.mark(0);
+    // one variant per key count (own view + k sender views)
+    const int32_t sl = in.my_slot;
+    if (k == 0) pv_merge_row<1>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 1) pv_merge_row<2>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 2) pv_merge_row<3>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 3) pv_merge_row<4>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 4) pv_merge_row<5>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 5) pv_merge_row<6>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else if (k == 6) pv_merge_row<7>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    else pv_merge_row<8>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    pm.mark(5);
+    pv_finish(a, sh, lr, k, k_all, false, ro);
     pm.mark(6);
-    (void)0;
 }
 
-// One lane per receiver row: the K smallest senders of its CSR segment, ascending.
+// Tick 0: every row writes its pre-joined bounded view {(r + 1 + j * (n / V)) mod n} (or
+// everyone if n - 1 <= V) with hb = h0, ts = 0.
+__global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
+    __shared__ PvShared sh;
+    const int32_t tid = threadIdx.x;
+    const int32_t lr = blockIdx.x, r = a.row0 + lr, V = a.view, n = a.n;
+    if (a.tick > a.fail_tick[r]) {
+        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
+        return;
+    }
+    RowOut ro{};
+    uint32_t *ids = sh.keys[0];
+    if (n - 1 <= V) {
+        for (int32_t x = tid; x < n; x += kPvBlock)
+            if (x != r) ids[x < r ? x : x - 1] = uint32_t(x);
+        ro.len = n - 1;
+    } else {
+        const int64_t stride = n / V;
+        const int64_t first_wrap = (int64_t(n) - r - 1 + stride - 1) / stride;
+        const int32_t J = int32_t(first_wrap < V ? first_wrap : V);
+        for (int32_t j = tid; j < V; j += kPvBlock) {
+            int64_t x = int64_t(r) + 1 + int64_t(j) * stride;
+            int32_t p;
+            if (x >= n) { x -= n; p = j - J; } else { p = j + (V - J); }
+            ids[p] = uint32_t(x);
+        }
+        ro.len = V;
+    }
+    for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
+    ro.ids_off = 0;
+    ro.vals_off = lds_half(sh, sh.vals);
+    __syncthreads();
+    pv_finish(a, sh, lr, 0, 0, true, ro);
+}
+
+// kWaves: minimum waves per SIMD the register allocation must allow (8 = 8 rows per CU, the
+// LDS limit; 7 = the allocator's own choice).  A/B switch: GSP_PV_WAVES.  One row per
+// workgroup: a software-pipelined variant (the next row's record, own view and first sender
+// views requested while the current row merged, two rows per workgroup) measured 4-8 % slower
+// -- other resident rows already hide the HBM round trips.
+template <int kWaves>
+__global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
+    __shared__ PvShared sh;
+    RowIn<1> in;
+    pv_load1(a, pv_row_of(a, int32_t(blockIdx.x)), in);
+    pv_row(a, sh, in, [] {});
+}
+
+// One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
+// a.kcount set, the rows are also bucketed by k (how many messages they merge): the tick
+// kernel then runs them k-descending, so each CU runs one code variant at a time.
 __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) {
     const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
-    if (lr >= a.rows) return;
-    const int32_t o0 = a.off[lr], k_all = a.off[lr + 1] - o0;
-    int32_t bs[8], bl[8];
+    const bool valid = lr < a.rows;
+    int32_t k = 0, k_all = 0;
+    if (valid) {
+        const int32_t o0 = a.off[lr];
+        k_all = a.off[lr + 1] - o0;
+        int32_t bs[8], bl[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
-    if (k_all > a.max_segment) {
-        atomicCAS(a.err, 0, a.tick);        // this tick's tick kernel sees it and runs no row
-    } else {
-        for (int32_t i = 0; i < k_all; ++i) {             // insertion into the sorted best 8
-            int32_t s = a.csr_src[o0 + i];
-            int32_t sl = a.csr_slot ? a.csr_slot[o0 + i] : s - a.row0;
+        for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
+        if (k_all > a.max_segment) {
+            atomicCAS(a.err, 0, a.tick);        // this tick's tick kernel sees it and runs no row
+        } else {
+            for (int32_t i = 0; i < k_all; ++i) {             // insertion into the sorted best 8
+                int32_t s = a.csr_src[o0 + i];
+                int32_t sl = a.csr_slot ? a.csr_slot[o0 + i] : s - a.row0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const bool lt = s < bs[q];
-                const int32_t ts = bs[q], tl = bl[q];
-                bs[q] = lt ? s : ts;
-                bl[q] = lt ? sl : tl;
-                s = lt ? ts : s;
-                sl = lt ? tl : sl;
+                for (int q = 0; q < 8; ++q) {
+                    const bool lt = s < bs[q];
+                    const int32_t ts = bs[q], tl = bl[q];
+                    bs[q] = lt ? s : ts;
+                    bl[q] = lt ? sl : tl;
+                    s = lt ? ts : s;
+                    sl = lt ? tl : sl;
+                }
             }
         }
+        k = k_all > a.max_segment ? 0 : (k_all < a.inbox ? k_all : a.inbox);
+        int4 *ps = reinterpret_cast<int4 *>(a.rc_src + int64_t(lr) * 8);
+        int4 *pl = reinterpret_cast<int4 *>(a.rc_slot + int64_t(lr) * 8);
+        ps[0] = make_int4(bs[0], bs[1], bs[2], bs[3]);
+        ps[1] = make_int4(bs[4], bs[5], bs[6], bs[7]);
+        pl[0] = make_int4(bl[0], bl[1], bl[2], bl[3]);
+        pl[1] = make_int4(bl[4], bl[5], bl[6], bl[7]);
+        a.rc_info[lr] = k | (k_all << 3);
     }
-    const int32_t k = k_all < a.inbox ? k_all : a.inbox;
-    int4 *ps = reinterpret_cast<int4 *>(a.rc_src + int64_t(lr) * 8);
-    int4 *pl = reinterpret_cast<int4 *>(a.rc_slot + int64_t(lr) * 8);
-    ps[0] = make_int4(bs[0], bs[1], bs[2], bs[3]);
-    ps[1] = make_int4(bs[4], bs[5], bs[6], bs[7]);
-    pl[0] = make_int4(bl[0], bl[1], bl[2], bl[3]);
-    pl[1] = make_int4(bl[4], bl[5], bl[6], bl[7]);
-    a.rc_info[lr] = (k_all > a.max_segment ? 0 : k) | (k_all << 3);
+    if (a.kcount) {        // block histogram of k, one global atomic per non-empty bucket
+        __shared__ int32_t s_cnt[8], s_base[8];
+        if (threadIdx.x < 8) s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const int32_t pos = valid ? atomicAdd(&s_cnt[k], 1) : 0;
+        __syncthreads();
+        if (threadIdx.x < 8 && s_cnt[threadIdx.x])
+            s_base[threadIdx.x] = atomicAdd(&a.kcount[threadIdx.x], s_cnt[threadIdx.x]);
+        __syncthreads();
+        if (valid) a.order[int64_t(k) * a.rows + s_base[k] + pos] = lr;
+    }
 }
 
 // Peers and sends of every row (one lane per row), after the tick kernel wrote the views:
@@ -814,7 +871,7 @@ void launch_send_and_digest(const PviewTickArgs &a, hipStream_t st) {
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st) {
     if (!pv_args_ok(a)) return hipErrorInvalidValue;
     if (a.rows == 0) return hipSuccess;
-    hipLaunchKernelGGL((pview_tick_kernel<true, 7>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    hipLaunchKernelGGL(pview_init_kernel, dim3(a.rows), dim3(kPvBlock), 0, st, a);
     launch_send_and_digest(a, st);
     return hipGetLastError();
 }
@@ -829,10 +886,9 @@ hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st) {
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     if (!pv_args_ok(a)) return hipErrorInvalidValue;
     if (a.rows == 0) return hipSuccess;
-    if (a.waves == 8)
-        hipLaunchKernelGGL((pview_tick_kernel<false, 8>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
-    else
-        hipLaunchKernelGGL((pview_tick_kernel<false, 7>), dim3(a.rows), dim3(kPvBlock), 0, st, a);
+    const dim3 g(unsigned(a.rows)), blk(kPvBlock);
+    if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8>), g, blk, 0, st, a);
+    else hipLaunchKernelGGL((pview_tick_kernel<7>), g, blk, 0, st, a);
     launch_send_and_digest(a, st);
     return hipGetLastError();
 }

@@ -43,6 +43,9 @@ struct PviewTickArgs {
     int32_t *err;                // [1] capacity error: 0, else the first tick a receiver was
                                  // sent more than max_segment messages (the job stops there)
     int32_t max_segment;         // <= kPvMaxSegment (lowered only by tests)
+    const int32_t *kcount;       // [8] rows per merged-message count k (or null: row order)
+    const int32_t *order;        // [8][rows]: the rows of each k; workgroup b runs the b-th row
+                                 // of the k-descending order (one code variant per CU stretch)
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
     int32_t waves;               // register budget variant of the tick kernel (7 or 8)
 };
@@ -54,6 +57,7 @@ struct PviewReceiptArgs {
     const int32_t *csr_slot;     // row mode: sender rows (null: local row = src - row0)
     int32_t rows, row0, inbox, tick, max_segment;
     int32_t *rc_info, *rc_src, *rc_slot;
+    int32_t *kcount, *order;     // k-bucketed row order for the tick kernel (or null)
     int32_t *err;
 };
 
