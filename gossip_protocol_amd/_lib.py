@@ -44,11 +44,43 @@ class GspExactStats(ctypes.Structure):
                 ("draws", c_int64), ("sends_admitted", c_int64), ("device_ms", ctypes.c_double)]
 
 
+MAX_FAIL_EVENTS = 8
+
+
+class GspFailEvent(ctypes.Structure):
+    _fields_ = [("tick", c_int32), ("mode", c_int32), ("ppm", c_int32)]
+
+
+class GspPolicy(ctypes.Structure):
+    """gsp_policy: driver policies of the scale engines (join schedule + bounded introducer
+    list, drop window, crash events); all zeros = off."""
+    _fields_ = [("drop_from", c_int32), ("drop_until", c_int32), ("step_rate", ctypes.c_double),
+                ("intro_list", c_int32), ("n_fail_events", c_int32),
+                ("fail_events", GspFailEvent * MAX_FAIL_EVENTS)]
+
+
+def make_policy(drop_window=None, step_rate=0.0, intro_list=0, fail_events=()):
+    """A GspPolicy: drop_window=(from, until), step_rate (node i starts at (int)(step_rate*i)),
+    intro_list (JOINREP payload bound), fail_events=[(tick, mode, ppm), ...]."""
+    p = GspPolicy()
+    if drop_window:
+        p.drop_from, p.drop_until = drop_window
+    p.step_rate = step_rate
+    p.intro_list = intro_list
+    if len(fail_events) > MAX_FAIL_EVENTS:
+        raise ValueError("at most %d failure events" % MAX_FAIL_EVENTS)
+    p.n_fail_events = len(fail_events)
+    for i, (tick, mode, ppm) in enumerate(fail_events):
+        p.fail_events[i] = GspFailEvent(tick, mode, ppm)
+    return p
+
+
 class GspScaleParams(ctypes.Structure):
     _fields_ = [("n", c_int32), ("fanout", c_int32), ("drop_pct", c_int32),
                 ("tremove", c_int32), ("h0", c_int32), ("fail_mode", c_int32),
                 ("fail_tick", c_int32), ("fail_ppm", c_int32), ("seed", c_uint64),
-                ("max_ticks", c_int32), ("tfail", c_int32), ("swim", c_int32)]
+                ("max_ticks", c_int32), ("tfail", c_int32), ("swim", c_int32),
+                ("policy", GspPolicy), ("events", c_int32), ("event_cap", c_int64)]
 
 
 class GspScaleDigest(ctypes.Structure):
@@ -67,7 +99,8 @@ class GspPviewParams(ctypes.Structure):
     _fields_ = [("n", c_int32), ("view", c_int32), ("fanout", c_int32), ("inbox", c_int32),
                 ("drop_pct", c_int32), ("tremove", c_int32), ("h0", c_int32),
                 ("fail_mode", c_int32), ("fail_tick", c_int32), ("fail_ppm", c_int32),
-                ("seed", c_uint64), ("max_ticks", c_int32)]
+                ("seed", c_uint64), ("max_ticks", c_int32), ("tfail", c_int32), ("swim", c_int32),
+                ("policy", GspPolicy), ("events", c_int32), ("event_cap", c_int64)]
 
 
 class GspPviewDigest(ctypes.Structure):
@@ -108,6 +141,9 @@ SIGNATURES = {
     "gsp_log_bytes": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
                                      P(ctypes.c_size_t)]),
     "gsp_exact_stats_get": (ctypes.c_int, [ctypes.c_void_p, P(GspExactStats)]),
+    "gsp_scale_params_from_conf": (ctypes.c_int, [ctypes.c_char_p, P(GspScaleParams)]),
+    "gsp_pview_params_from_conf": (ctypes.c_int, [ctypes.c_char_p, P(GspPviewParams)]),
+    "gsp_struct_size": (c_int64, [ctypes.c_char_p]),
     "gsp_scale_create": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, P(ctypes.c_void_p)]),
     "gsp_scale_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "gsp_scale_step": (ctypes.c_int, [ctypes.c_void_p, c_int32]),

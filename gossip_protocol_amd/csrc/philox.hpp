@@ -16,7 +16,22 @@ enum : uint32_t {
     kDomainFail = 0x4641494Cu,  // "FAIL": failure injection
     kDomainPeer = 0x50454552u,  // "PEER": scale-mode peer choice
     kDomainPing = 0x50494E47u,  // "PING": SWIM probe target and probe paths
+    kDomainJoin = 0x4A4F494Eu,  // "JOIN": the members a JOINREP carries (bounded introducer list)
 };
+
+// Sequential sampling without replacement: draw k maps u % (cnt - k) onto the ranks not
+// chosen yet, in ascending order (chosen[] kept sorted).  Used for peers, probe targets and
+// the bounded introducer list alike; identical on host and device, in every lane.
+__host__ __device__ inline int32_t next_distinct_rank(uint32_t u, int32_t cnt, int32_t k,
+                                                      int32_t *chosen, int32_t &nch) {
+    int32_t rk = int32_t(u % uint32_t(cnt - k));
+    int32_t pos = 0;
+    while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
+    for (int32_t q = nch; q > pos; --q) chosen[q] = chosen[q - 1];
+    chosen[pos] = rk;
+    nch++;
+    return rk;
+}
 
 __host__ __device__ inline uint32_t philox_word0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                  uint32_t k0, uint32_t k1) {

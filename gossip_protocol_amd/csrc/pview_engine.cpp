@@ -23,15 +23,14 @@
 #include <vector>
 
 #include "common.hpp"
+#include "join_kernels.hpp"
 #include "philox.hpp"
+#include "policy.hpp"
 #include "pview_kernels.hpp"
 #include "rowx_host.hpp"
 #include "rowx_kernels.hpp"
 #include "scale_kernels.hpp"
 
-namespace gsp {
-std::vector<int32_t> scale_fail_ticks(const gsp_scale_params &p);
-}
 
 namespace {
 
@@ -39,15 +38,18 @@ struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
-        tile_sum, rc_info, rc_src, rc_slot, kcount, order;
+        tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok;
+    gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     gsp::RowxBufs x;             // row exchange (G > 1)
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
         for (auto *b : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &err,
-                        &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order})
+                        &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order, &start_tick, &ping,
+                        &joiners, &join_ok})
             b->release();
+        intro_buf.release();
         x.release();
         dig.release();
         prof.release();
@@ -73,7 +75,9 @@ struct gsp_pview {
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
-    std::vector<int32_t> h_fail;
+    std::vector<int32_t> h_fail, h_start;
+    bool joins = false;          // a join schedule is set (some node starts after tick 0)
+    gsp::JoinPlan plan;
     int32_t *h_cnt = nullptr;    // pinned [G][2G]: pair counts then record counts per shard
     int32_t *h_recv = nullptr;   // pinned [local][G]: records each local shard receives
     struct Timed { hipEvent_t a, b, c; };
@@ -103,12 +107,19 @@ struct gsp_pview {
         a.fanout = p.fanout;
         a.tick = t;
         a.tremove = p.tremove;
-        a.drop_pct = p.drop_pct;
         a.h0 = p.h0;
         a.row0 = sh.row0;
         a.rows = sh.rows;
         a.seed = p.seed;
         a.fail_tick = sh.fail_tick.p;
+        a.start_tick = joins ? sh.start_tick.p : nullptr;
+        a.drop_pct = gsp::drop_at(p.policy, p.drop_pct, t);
+        a.drop_prev = gsp::drop_at(p.policy, p.drop_pct, t - 1);
+        a.tfail = p.tfail;
+        a.swim = p.swim;
+        a.ping = sh.ping.p;
+        a.intro = (rowmode && sh.row0 != 0) ? sh.intro_buf.p : sh.table[(t + 1) & 1].p;
+        a.intro_list = p.policy.intro_list;
         a.own_hb = sh.own_hb.p;
         a.len_cur = sh.len[t & 1].p;
         a.rc_info = sh.rc_info.p;
@@ -171,7 +182,12 @@ int pview_validate(const gsp_pview_params *p) {
     GSP_REQUIRE(p->fail_mode >= 0 && p->fail_mode <= 2, GSP_ERR_INVALID, "fail_mode=%d", p->fail_mode);
     GSP_REQUIRE(p->max_ticks >= 1 && int64_t(p->h0) + p->max_ticks <= 2047, GSP_ERR_RANGE,
                 "h0 + max_ticks exceeds the 11-bit packed heartbeat");
-    return GSP_OK;
+    GSP_REQUIRE(p->tfail == 0 || (p->tfail >= 1 && p->tfail < p->tremove), GSP_ERR_INVALID,
+                "tfail=%d: 0 (off) or 1..tremove-1", p->tfail);
+    GSP_REQUIRE(p->swim >= 0 && p->swim <= 8, GSP_ERR_INVALID, "swim=%d: 0 (off) or 1..8 paths", p->swim);
+    GSP_REQUIRE(p->events == 0 || p->events == 1, GSP_ERR_INVALID, "events=%d", p->events);
+    GSP_REQUIRE(p->event_cap >= 0, GSP_ERR_INVALID, "event_cap=%lld", (long long)p->event_cap);
+    return gsp::validate_policy(p->policy, p->n);
 }
 
 int shard_alloc(gsp_pview *s, PvShard &sh) {
@@ -203,6 +219,23 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     GSP_HIP(hipMemsetAsync(sh.rowdig.p, 0, rows * 16 * 8, st));
     if (s->rowmode)
         GSP_HIP(sh.x.alloc(G, s->pair_cap, s->msg_cap, V, int64_t(n) * F, st));
+    if (s->p.swim > 0) {
+        GSP_HIP(sh.ping.alloc(rows));
+        GSP_HIP(hipMemsetAsync(sh.ping.p, 0xFF, rows * 4, st));     // -1: no probe yet
+    }
+    if (s->joins) {
+        GSP_HIP(sh.start_tick.alloc(size_t(n)));
+        GSP_HIP(hipMemcpyAsync(sh.start_tick.p, s->h_start.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
+        const size_t nj = std::max<size_t>(1, s->plan.joiners.size());
+        GSP_HIP(sh.joiners.alloc(nj));
+        GSP_HIP(sh.join_ok.alloc(nj));
+        if (!s->plan.joiners.empty())
+            GSP_HIP(hipMemcpyAsync(sh.joiners.p, s->plan.joiners.data(), s->plan.joiners.size() * 4,
+                                   hipMemcpyHostToDevice, st));
+        // a late joiner's (empty) view is read at its start tick from either buffer
+        GSP_HIP(hipMemsetAsync(sh.table[1].p, 0xFF, rows * size_t(V) * 8, st));
+        if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(V)));
+    }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
@@ -237,6 +270,56 @@ int pview_mirrored_err(gsp_pview *s) {
         GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
                     "a receiver was sent more than %d messages at tick %d; the job stopped there",
                     s->max_segment, s->h_err[i]);
+    return GSP_OK;
+}
+
+// The JOINREPs node 0 sends at tick t to the nodes that start at t + 1 (join_kernels.hpp),
+// and (row layout) node 0's view of tick t broadcast to the other shards as their payload.
+int pv_join_sends(gsp_pview *s, int32_t t) {
+    const int64_t cnt = s->plan.count(t + 1);
+    if (!s->joins || cnt == 0) return GSP_OK;
+    for (PvShard &sh : s->local) {
+        gsp::JoinSendArgs j{};
+        j.joiners = sh.joiners.p + s->plan.first(t + 1);
+        j.count = int32_t(cnt);
+        j.tick = t;
+        j.drop_pct = gsp::drop_at(s->p.policy, s->p.drop_pct, t);
+        j.seed = s->p.seed;
+        j.fail_tick = sh.fail_tick.p;
+        j.lo = sh.row0;
+        j.hi = sh.row0 + sh.rows;
+        j.ok = sh.join_ok.p + s->plan.first(t + 1);
+        j.deg = sh.deg.p;
+        unsigned long long *dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
+        j.sent = dig + gsp::kPvSent;
+        j.dropped = dig + gsp::kPvDropped;
+        GSP_HIP(gsp::launch_join_send(j, s->st));
+    }
+    if (!s->rowmode || s->shards == 1) return GSP_OK;
+    const size_t bytes = size_t(s->p.view) * 8;
+    if (s->comm) {
+        PvShard &sh = s->local[0];
+        void *buf = sh.row0 == 0 ? static_cast<void *>(sh.table[t & 1].p) : static_cast<void *>(sh.intro_buf.p);
+        GSP_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, 0, s->comm, s->st));
+        s->perf.xgmi_bytes += sh.row0 == 0 ? double(bytes) * double(s->shards - 1) : 0.0;
+        return GSP_OK;
+    }
+    const PvShard &root = s->local[0];
+    for (PvShard &sh : s->local)
+        if (sh.row0 != 0) {
+            GSP_HIP(hipMemcpyAsync(sh.intro_buf.p, root.table[t & 1].p, bytes, hipMemcpyDeviceToDevice, s->st));
+            s->perf.xgmi_bytes += double(bytes);
+        }
+    return GSP_OK;
+}
+
+int pv_join_scatter(gsp_pview *s, int32_t t) {
+    const int64_t cnt = s->plan.count(t);
+    if (!s->joins || cnt == 0) return GSP_OK;
+    for (PvShard &sh : s->local)
+        GSP_HIP(gsp::launch_join_scatter(sh.joiners.p + s->plan.first(t), sh.join_ok.p + s->plan.first(t),
+                                         int32_t(cnt), sh.row0, sh.rows, sh.off.p, sh.fill.p, sh.csr_src.p,
+                                         s->rowmode ? sh.x.csr_slot.p : nullptr, s->st));
     return GSP_OK;
 }
 
@@ -279,10 +362,10 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
-    gsp_scale_params fp{};
-    fp.n = p->n; fp.fail_mode = p->fail_mode; fp.fail_tick = p->fail_tick;
-    fp.fail_ppm = p->fail_ppm; fp.seed = p->seed;
-    s->h_fail = gsp::scale_fail_ticks(fp);
+    s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
+    s->h_start = gsp::start_ticks(p->policy, p->n);
+    s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
+    if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
     int32_t max_rows = 0;
     for (int32_t g = 0; g < shards; ++g)
         max_rows = std::max(max_rows, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
@@ -311,6 +394,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         if (int rc = shard_alloc(s.get(), sh)) return rc;
     }
     for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_init(s->args(sh, 0), s->st));
+    if (int rc = pv_join_sends(s.get(), 0)) return rc;
     GSP_HIP(hipStreamSynchronize(s->st));
     *out = s.release();
     return GSP_OK;
@@ -404,6 +488,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
                                         sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
             GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
         }
+        if (int rc = pv_join_scatter(s, t)) return rc;
         for (PvShard &sh : s->local) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
@@ -414,6 +499,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);
         }
+        if (int rc = pv_join_sends(s, t)) return rc;
         s->tick = t;
         s->perf.ticks++;
     }

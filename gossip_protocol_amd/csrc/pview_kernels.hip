@@ -26,6 +26,7 @@
 //      peers; the row's digest counts go to a per-row record (no global atomics), summed by
 //      pview_digest_kernel.
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
+#include "join_kernels.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
 #include "wave_ops.hpp"
@@ -188,11 +189,13 @@ struct RowOut {
 
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
-template <int kBlocks, int kPre, typename Mid>
+// jrep: message 1 is a JOINREP (its payload: node 0's view cut to the bounded introducer
+// list); pcol / pok: the SWIM probe of t - 1 (target id or kNoId, answered).
+template <int kBlocks>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
-                                             int32_t k, const uint64_t (&pre)[kPre],
-                                             int32_t my_slot, const uint32_t (&ssrc)[kPvMaxInbox],
-                                             RowOut &ro, PvMark &pm, Mid &&mid) {
+                                             int32_t k, uint64_t ent0, int32_t my_slot,
+                                             const uint32_t (&ssrc)[kPvMaxInbox], bool jrep,
+                                             uint32_t pcol, bool pok, RowOut &ro, PvMark &pm) {
     constexpr int Q = kBlocks;                           // keys per lane
     constexpr int kJ = kBlocks - 1;                      // k <= kJ messages in this variant
     constexpr int P = kBlocks * kSlots;
@@ -205,22 +208,42 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                    S_evict = pv_seed(3, t, uint32_t(r));
 
     // ---- 2. keys: one sorted block of 256 slots per source ------------------------------------
-    // entries [0, kPre) arrived with the row (the own view slot), the sender views are
-    // requested here (one coalesced 2 KB view each)
+    // block 0 = the own view (loaded with the record), block m = message m's payload: the
+    // sender's view (one coalesced 2 KB load) cut to what it gossiped at t - 1 (TFAIL), or for
+    // a JOINREP node 0's view cut to the Philox-chosen members (bounded introducer list)
+    const uint32_t tf = uint32_t(a.tfail), t5m1 = (t - 1u) & 31u;
+    auto gossiped = [&](uint64_t v) {      // listed, and not suspected when sent at t - 1
+        return v != kPvEmpty && (tf == 0 || ((t5m1 - uint32_t(v)) & 31u) < tf);
+    };
     uint64_t ent[kBlocks];
+    ent[0] = ent0;
 #pragma unroll
-    for (int m = 0; m < kBlocks; ++m) {
-        if (m < kPre) { ent[m] = pre[m < kPre ? m : 0]; continue; }
+    for (int m = 1; m < kBlocks; ++m) {
         ent[m] = kPvEmpty;
         if (m <= k && tid < V) {
             const int32_t sl = __builtin_amdgcn_readlane(my_slot, m - 1);
-#ifdef GSP_PV_EXP_L2   // timing experiment only (wrong results): sender views from 64 hot rows
-            const uint64_t *row = a.prev + int64_t(sl & 63) * V;
-#else
-            const uint64_t *row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
-#endif
+            const uint64_t *row = (m == 1 && jrep) ? a.intro
+                                  : sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
             ent[m] = __builtin_nontemporal_load(row + tid);
+            if (!gossiped(ent[m])) ent[m] = kPvEmpty;
         }
+    }
+    if constexpr (kBlocks > 1) if (jrep) {   // block-uniform: rank node 0's gossiped members
+        const bool g = ent[1] != kPvEmpty;
+        uint32_t cnt0 = 0;
+        const uint32_t rank = block_scan(g ? 1u : 0u, &cnt0, sh.keys[1]);   // keys[1] is free here
+        const int32_t B = a.intro_list < int32_t(cnt0) ? a.intro_list : int32_t(cnt0);
+        int32_t ranks[kMaxIntro];
+        int32_t nch = 0;
+        bool chosen = false;
+        for (int32_t i = 0; i < B; ++i) {
+            const int32_t rk = next_distinct_rank(
+                draw_u31(kDomainJoin, a.seed, t - 1u, 0u, uint32_t(r), uint32_t(i)), int32_t(cnt0), i,
+                ranks, nch);
+            (void)rk;
+        }
+        for (int32_t i = 0; i < nch; ++i) chosen = chosen || (g && uint32_t(ranks[i]) == rank);
+        if (!chosen) ent[1] = kPvEmpty;
     }
     uint32_t merged = 0;                                 // payload entries (MP1Node.cpp:245 trips)
 #pragma unroll
@@ -233,7 +256,6 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
     }
     __syncthreads();
-    mid();                    // the next row's sender-view loads go out here (pipelined kernel)
     pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
@@ -349,6 +371,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (!aown) continue;
         if (ajs && !adone) av = pv_event(av, t5);
         if (x == uint32_t(r) || !av) continue;                  // never list yourself
+        if (x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
         if (!ae0) { joins++; hsum += pv_hash(S_join, x); }
         if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
@@ -581,7 +604,9 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
         uint64_t w0 = mg, w1 = jr | (ev << 32);
         if (wave == 0) {
             a.len_cur[lr] = len;
-            a.own_hb[lr] = int32_t(t);               // alive at every tick 1..t (pre-joined)
+            // alive at every tick since it started (pre-joined: ticks 1..t)
+            const int32_t st = a.start_tick ? a.start_tick[a.row0 + lr] : 0;
+            a.own_hb[lr] = int32_t(t) - (st > 0 ? st - 1 : 0);
             w0 += uint64_t(k) | (uint64_t(k) << 32) | (1ull << 56);
             w1 |= uint64_t(k_all - k) << 48;
         }
@@ -591,14 +616,6 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
         else rec[1] = make_ulonglong2(h, 0ull);
     }
 }
-
-// What a row needs before its merge starts: the receipt record and its first kPre entries
-// (the own view slot); the sender views are loaded by the merge.
-template <int kPre>
-struct RowIn {
-    int32_t lr, info, my_src, my_slot;
-    uint64_t ent[kPre];
-};
 
 // workgroup-order index b -> row: b itself, or the b-th row of the k-descending order
 __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) {
@@ -612,49 +629,57 @@ __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) 
     return a.order[int64_t(q) * a.rows + b];
 }
 
-// stage 1: the own view slot and the receipt record (independent loads)
-template <int kPre>
-__device__ __forceinline__ void pv_load1(const PviewTickArgs &a, int32_t lr, RowIn<kPre> &in) {
+// One non-init row: the own view slot and the receipt record are requested first (their
+// latencies overlap), then merge, ops, eviction, view write and digest record.
+__device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int32_t lr) {
     const int32_t tid = threadIdx.x, lane = tid & 63;
-    in.lr = lr;
-    in.ent[0] = tid < a.view ? __builtin_nontemporal_load(a.prev + int64_t(lr) * a.view + tid) : kPvEmpty;
-    in.info = a.rc_info[lr];
-    in.my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
-    in.my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
-}
-
-// One non-init row from its record: merge, ops, eviction, view write, digest record.
-// mid() runs once on every path (after the key build, or at once for a row that does not run).
-template <int kPre, typename Mid>
-__device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, const RowIn<kPre> &in,
-                                       Mid &&mid) {
-    const int32_t tid = threadIdx.x;
-    const int32_t lr = in.lr, r = a.row0 + lr;
-    if (a.tick > a.fail_tick[r] || *a.err) {   // crashed (no recv, no ops, no send), or a
-        mid();                                 // capacity error stopped the job
+    const int32_t r = a.row0 + lr;
+    const uint64_t ent0 = tid < a.view ? __builtin_nontemporal_load(a.prev + int64_t(lr) * a.view + tid)
+                                       : kPvEmpty;
+    const int32_t info_v = a.rc_info[lr];
+    const int32_t my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
+    const int32_t my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
+    // crashed (no recv, no ops, no send), not started yet, or a capacity error stopped the job
+    if (a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) || *a.err) {
         if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
         return;
     }
     PvMark pm;
     pm.init(a.prof);
     RowOut ro{};
-    const int32_t info = __builtin_amdgcn_readfirstlane(in.info);
+    const int32_t info = __builtin_amdgcn_readfirstlane(info_v);
     const int32_t k = info & 7, k_all = info >> 3;
+    // a JOINREP (sender kJoinRepSrc) sorts first; its sender event is node 0's
+    const bool jrep = k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
     uint32_t ssrc[kPvMaxInbox];
 #pragma unroll
     for (int jj = 0; jj < kPvMaxInbox; ++jj)
-        ssrc[jj] = jj < k ? uint32_t(__builtin_amdgcn_readlane(in.my_src, jj)) : kNoId;
+        ssrc[jj] = jj < k ? uint32_t(__builtin_amdgcn_readlane(my_src, jj)) : kNoId;
+    if (jrep) ssrc[0] = 0u;
+    // SWIM: the probe this row sent at t - 1, answered iff its target is alive now and one of
+    // the swim paths survived its drop draw (paths sent at t - 1)
+    uint32_t pcol = kNoId;
+    bool pok = false;
+    if (a.swim > 0) {
+        const int32_t p = __builtin_amdgcn_readfirstlane(a.ping[lr]);
+        if (p >= 0) {
+            pcol = uint32_t(p);
+            for (int32_t i = 0; i < a.swim; ++i)
+                pok = pok || int32_t(draw_u31(kDomainPing, a.seed, uint32_t(a.tick - 1), uint32_t(r),
+                                              uint32_t(p), uint32_t(i)) % 100u) >= a.drop_prev;
+            pok = pok && a.tick <= a.fail_tick[p] && (!a.start_tick || a.tick >= a.start_tick[p]);
+        }
+    }
     pm.mark(0);
     // one variant per key count (own view + k sender views)
-    const int32_t sl = in.my_slot;
-    if (k == 0) pv_merge_row<1>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 1) pv_merge_row<2>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 2) pv_merge_row<3>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 3) pv_merge_row<4>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 4) pv_merge_row<5>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 5) pv_merge_row<6>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else if (k == 6) pv_merge_row<7>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
-    else pv_merge_row<8>(a, sh, r, k, in.ent, sl, ssrc, ro, pm, mid);
+    if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 2) pv_merge_row<3>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 3) pv_merge_row<4>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 4) pv_merge_row<5>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 5) pv_merge_row<6>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 6) pv_merge_row<7>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else pv_merge_row<8>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
     pm.mark(5);
     pv_finish(a, sh, lr, k, k_all, false, ro);
     pm.mark(6);
@@ -688,8 +713,19 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
         }
         ro.len = V;
     }
-    for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
     ro.ids_off = 0;
+    if (a.start_tick) {        // join schedule: only the nodes that start at tick 0 are listed
+        __syncthreads();
+        const bool late = a.start_tick[r] > 0;
+        const uint32_t x = tid < ro.len ? ids[tid] : 0u;
+        const bool keep = tid < ro.len && !late && a.start_tick[x] == 0;
+        uint32_t total = 0;
+        const uint32_t pos = block_scan(keep ? 1u : 0u, &total, sh.keys[1]);
+        if (keep) sh.keys[1][8 + pos] = x;
+        ro.len = int32_t(total);
+        ro.ids_off = lds_word(sh, sh.keys[1] + 8);       // keys[1][8 ..): the kept ids
+    }
+    for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
     ro.vals_off = lds_half(sh, sh.vals);
     __syncthreads();
     pv_finish(a, sh, lr, 0, 0, true, ro);
@@ -703,9 +739,7 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
 template <int kWaves>
 __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared sh;
-    RowIn<1> in;
-    pv_load1(a, pv_row_of(a, int32_t(blockIdx.x)), in);
-    pv_row(a, sh, in, [] {});
+    pv_row(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
 }
 
 // One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
@@ -768,16 +802,50 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     const int32_t r = a.row0 + lr, F = a.fanout;
     const uint32_t t = uint32_t(a.tick);
     unsigned long long *w3 = a.rowdig + int64_t(lr) * 16 + 3;
-    const bool dead = a.tick > a.fail_tick[r] || (a.tick > 0 && *a.err);
+    const bool dead = a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) ||
+                      (a.tick > 0 && *a.err);
     int32_t *od = a.out_dst + int64_t(lr) * F;
     if (dead) {
         for (int32_t q = 0; q < F; ++q) od[q] = -1;
+        if (a.swim > 0) a.ping[lr] = -1;
         *w3 = 0ull;
         return;
     }
     const int32_t len = a.len_cur[lr];
-    const int32_t keff = F < len ? F : len;
     const uint64_t *row = a.cur + int64_t(lr) * a.view;
+    // TFAIL: peers and the probe target are chosen among the members not suspected at t,
+    // by rank in id order (an 8-word bitmap of the gossipable slots)
+    uint32_t gmask[kPvMaxView / 32];
+    int32_t cnt = len;
+    if (a.tfail > 0) {
+        cnt = 0;
+        const uint32_t t5 = t & 31u, tf = uint32_t(a.tfail);
+#pragma unroll
+        for (int w = 0; w < kPvMaxView / 32; ++w) {
+            uint32_t m = 0;
+            for (int b = 0; b < 32; ++b) {
+                const int32_t i = w * 32 + b;
+                if (i < len && ((t5 - uint32_t(row[i])) & 31u) < tf) m |= 1u << b;
+            }
+            gmask[w] = m;
+            cnt += __builtin_popcount(m);
+        }
+    }
+    auto slot_of = [&](int32_t rk) -> int32_t {     // rank among the gossipable -> slot
+        if (a.tfail <= 0) return rk;
+#pragma unroll
+        for (int w = 0; w < kPvMaxView / 32; ++w) {
+            const int32_t c = __builtin_popcount(gmask[w]);
+            if (rk < c) {
+                uint32_t m = gmask[w];
+                for (int32_t z = 0; z < rk; ++z) m &= m - 1;
+                return w * 32 + __builtin_ffs(m) - 1;
+            }
+            rk -= c;
+        }
+        return 0;
+    };
+    const int32_t keff = F < cnt ? F : cnt;
     int32_t ch[16], dst[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) { ch[q] = 0x7FFFFFFF; dst[q] = -1; }
@@ -785,7 +853,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     for (int kk = 0; kk < 16; ++kk) {
         if (kk >= keff) continue;
         const uint32_t u = draw_u31(kDomainPeer, a.seed, t, uint32_t(r), uint32_t(kk), 0u);
-        int32_t rk = int32_t(u % uint32_t(len - kk));
+        int32_t rk = int32_t(u % uint32_t(cnt - kk));
 #pragma unroll
         for (int q = 0; q < 16; ++q) rk += (q < kk && rk >= ch[q]) ? 1 : 0;   // ch ascending
         int32_t x = rk;
@@ -796,7 +864,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
             ch[q] = lt ? x : c;
             x = lt ? c : x;
         }
-        dst[kk] = int32_t(row[rk] >> 32);
+        dst[kk] = int32_t(row[slot_of(rk)] >> 32);
     }
     uint32_t dropped = 0;
 #pragma unroll
@@ -809,6 +877,13 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
         }
         od[kk] = d;
         if (d >= 0) atomicAdd(&a.deg[d], 1);
+    }
+    if (a.swim > 0) {          // this tick's probe target: one more rank over the same order
+        int32_t p = -1;
+        if (cnt > 0)
+            p = int32_t(row[slot_of(int32_t(draw_u31(kDomainPing, a.seed, t, uint32_t(r), 0u, 0x100u) %
+                                            uint32_t(cnt)))] >> 32);
+        a.ping[lr] = p;
     }
     *w3 = uint64_t(keff) | (uint64_t(dropped) << 8);
 }

@@ -31,6 +31,12 @@ struct PviewTickArgs {
     int32_t row0, rows;
     uint64_t seed;
     const int32_t *fail_tick;    // [n]
+    const int32_t *start_tick;   // [n], or null: every node starts at tick 0 (policy.hpp)
+    int32_t drop_prev;           // drop percentage of the sends of tick - 1 (SWIM probe paths)
+    int32_t tfail, swim;         // TFAIL suspicion / SWIM probing (0: off), as the full view
+    int32_t *ping;               // swim: [rows] probe target chosen at the last send (-1 none)
+    const uint64_t *intro;       // node 0's view of tick - 1: the JOINREP payload source
+    int32_t intro_list;          // JOINREP payload bound B
     int32_t *own_hb;             // [rows]
     int32_t *len_cur;            // [rows] view length of this tick
     const int32_t *rc_info;      // [rows] receipt record: k | k_all << 3

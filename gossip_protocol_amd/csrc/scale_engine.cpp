@@ -21,7 +21,9 @@
 #include <vector>
 
 #include "common.hpp"
+#include "join_kernels.hpp"
 #include "philox.hpp"
+#include "policy.hpp"
 #include "rowx_host.hpp"
 #include "scale_kernels.hpp"
 
@@ -34,15 +36,17 @@ struct Shard {
     gsp::RowxBufs x;               // row layout exchange buffers
     gsp::DevBuf<uint16_t> table[2];
     gsp::DevBuf<int32_t> own_hb, fail_tick, cnt_total[2], cnt_slice, cnt_all, out_dst, picks,
-        ping, deg, off, fill, csr_src, err, tile_sum;
+        ping, deg, off, fill, csr_src, err, tile_sum, start_tick, joiners, join_ok;
+    gsp::DevBuf<uint16_t> intro_buf;   // row layout, shards != 0: node 0's row of the last tick
     gsp::DevBuf<uint8_t> bitmap;
     gsp::DevBuf<unsigned long long> dig;
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
         for (auto *x : {&own_hb, &fail_tick, &cnt_slice, &cnt_all, &out_dst, &picks, &ping, &deg, &off,
-                        &fill, &csr_src, &err, &tile_sum})
+                        &fill, &csr_src, &err, &tile_sum, &start_tick, &joiners, &join_ok})
             x->release();
+        intro_buf.release();
         bitmap.release();
         dig.release();
         x.release();
@@ -72,7 +76,9 @@ struct gsp_scale {
     int policy = 5;            // bit 0 nt own row, bit 1 nt sender rows, bit 2 pipelined loads
     int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
     std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
-    std::vector<int32_t> h_fail;
+    std::vector<int32_t> h_fail, h_start;
+    bool joins = false;        // a join schedule is set (some node starts after tick 0)
+    gsp::JoinPlan plan;        // the joiners of every start tick
     struct Timed { hipEvent_t a, b, c; };
     std::vector<Timed> pending;
     std::vector<hipEvent_t> free_events;
@@ -102,7 +108,6 @@ struct gsp_scale {
         a.tick = t;
         a.tremove = p.tremove;
         a.fanout = p.fanout;
-        a.drop_pct = p.drop_pct;
         a.h0 = p.h0;
         a.nt_own = policy & 1;
         a.nt_src = (policy >> 1) & 1;
@@ -112,6 +117,16 @@ struct gsp_scale {
         a.count_rounds = rowmode || sh.g == 0;
         a.seed = p.seed;
         a.fail_tick = sh.fail_tick.p;
+        a.start_tick = joins ? sh.start_tick.p : nullptr;
+        a.drop_pct = gsp::drop_at(p.policy, p.drop_pct, t);
+        a.drop_prev = gsp::drop_at(p.policy, p.drop_pct, t - 1);
+        // node 0's row of tick t - 1 (the JOINREP payload): the local row 0, or the copy the
+        // row layout's shard 0 broadcast
+        a.intro = (rowmode && sh.row0 != 0) ? sh.intro_buf.p : sh.table[(t + 1) & 1].p;
+        a.intro_list = p.policy.intro_list;
+        a.intro_cnt = sliced ? sh.cnt_all.p : nullptr;
+        a.shards = shards;
+        a.shard = sh.g;
         a.own_hb = sh.own_hb.p;
         a.cnt_prev = sh.cnt_total[(t + 1) & 1].p;
         a.cnt_cur = sliced ? sh.cnt_slice.p : sh.cnt_total[t & 1].p;
@@ -133,13 +148,14 @@ struct gsp_scale {
         r.n = p.n;
         r.fanout = p.fanout;
         r.tick = t;
-        r.drop_pct = p.drop_pct;
         r.shard = sh.g;
         r.shards = shards;
         r.count_rounds = sh.g == 0;
         r.stride = stride;
         r.seed = p.seed;
         r.fail_tick = sh.fail_tick.p;
+        r.start_tick = joins ? sh.start_tick.p : nullptr;
+        r.drop_pct = gsp::drop_at(p.policy, p.drop_pct, t);
         r.cnt_all = sh.cnt_all.p;
         r.cnt_total = sh.cnt_total[t & 1].p;
         r.bitmap = sh.bitmap.p;
@@ -155,21 +171,9 @@ struct gsp_scale {
 
 namespace gsp {
 
-// Failure schedule: the same Philox draws as the oracle (DESIGN.md "Scale mode").
+// Failure schedule: the same Philox draws as the oracle (policy.hpp; DESIGN.md "Scale mode").
 std::vector<int32_t> scale_fail_ticks(const gsp_scale_params &p) {
-    std::vector<int32_t> f(size_t(p.n), 0x7FFFFFFF);
-    if (p.fail_mode == 1) {
-        for (int32_t r = 0; r < p.n; ++r)
-            if (draw_u31(kDomainFail, p.seed, uint32_t(p.fail_tick), uint32_t(r), 0, 0) % 1000000u <
-                uint32_t(p.fail_ppm))
-                f[size_t(r)] = p.fail_tick;
-    } else if (p.fail_mode == 2) {
-        const int64_t m = int64_t(p.n) * p.fail_ppm / 1000000;
-        const uint32_t start = draw_u31(kDomainFail, p.seed, uint32_t(p.fail_tick), 0xFFFFFFFFu, 0, 0) %
-                               uint32_t(p.n);
-        for (int64_t i = 0; i < m; ++i) f[size_t((start + i) % uint32_t(p.n))] = p.fail_tick;
-    }
-    return f;
+    return fail_ticks(p.policy, p.n, p.seed, p.fail_mode, p.fail_tick, p.fail_ppm);
 }
 
 int validate_scale_params(const gsp_scale_params *p) {
@@ -189,7 +193,9 @@ int validate_scale_params(const gsp_scale_params *p) {
     GSP_REQUIRE(p->max_ticks >= 1 && int64_t(p->h0) + p->max_ticks <= 2047, GSP_ERR_RANGE,
                 "h0 + max_ticks = %d exceeds the 11-bit packed heartbeat (2047)",
                 p->h0 + p->max_ticks);
-    return GSP_OK;
+    GSP_REQUIRE(p->events == 0 || p->events == 1, GSP_ERR_INVALID, "events=%d", p->events);
+    GSP_REQUIRE(p->event_cap >= 0, GSP_ERR_INVALID, "event_cap=%lld", (long long)p->event_cap);
+    return validate_policy(p->policy, p->n);
 }
 
 }  // namespace gsp
@@ -231,6 +237,19 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(sh.dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
+    if (s->joins) {
+        GSP_HIP(sh.start_tick.alloc(size_t(n)));
+        GSP_HIP(hipMemcpyAsync(sh.start_tick.p, s->h_start.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
+        const size_t nj = std::max<size_t>(1, s->plan.joiners.size());
+        GSP_HIP(sh.joiners.alloc(nj));
+        GSP_HIP(sh.join_ok.alloc(nj));
+        if (!s->plan.joiners.empty())
+            GSP_HIP(hipMemcpyAsync(sh.joiners.p, s->plan.joiners.data(), s->plan.joiners.size() * 4,
+                                   hipMemcpyHostToDevice, st));
+        // a late joiner's row is read (empty) at its start tick from either buffer
+        GSP_HIP(hipMemsetAsync(sh.table[1].p, 0, tab * sizeof(uint16_t), st));
+        if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(s->stride)));
+    }
     GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
     GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, st));
     GSP_HIP(hipMemsetAsync(sh.err.p, 0, 4, st));
@@ -341,6 +360,61 @@ int check_err(gsp_scale *s) {
     return mirrored_err(s);
 }
 
+// The JOINREPs node 0 sends at tick t to the nodes that start at t + 1 (join_kernels.hpp):
+// deg of the receivers (next tick's CSR) and the digest's sent / dropped of tick t; the row
+// layout also broadcasts node 0's row of tick t to the other shards (the JOINREP payload).
+int join_sends(gsp_scale *s, int32_t t) {
+    const int64_t cnt = s->plan.count(t + 1);
+    if (!s->joins || cnt == 0) return GSP_OK;
+    for (Shard &sh : s->local) {
+        gsp::JoinSendArgs j{};
+        j.joiners = sh.joiners.p + s->plan.first(t + 1);
+        j.count = int32_t(cnt);
+        j.tick = t;
+        j.drop_pct = gsp::drop_at(s->p.policy, s->p.drop_pct, t);
+        j.seed = s->p.seed;
+        j.fail_tick = sh.fail_tick.p;
+        j.lo = s->rowmode ? sh.row0 : 0;
+        j.hi = s->rowmode ? sh.row0 + sh.rows : s->p.n;
+        j.ok = sh.join_ok.p + s->plan.first(t + 1);
+        j.deg = sh.deg.p;
+        const bool counts = s->rowmode || sh.g == 0;
+        unsigned long long *dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
+        j.sent = counts ? dig + gsp::kDigSent : nullptr;
+        j.dropped = counts ? dig + gsp::kDigDropped : nullptr;
+        GSP_HIP(gsp::launch_join_send(j, s->st));
+    }
+    if (!s->rowmode || s->shards == 1) return GSP_OK;
+    // node 0's row of tick t -> intro_buf of every other shard
+    const size_t bytes = size_t(s->stride) * sizeof(uint16_t);
+    if (s->comm) {
+        Shard &sh = s->local[0];
+        void *buf = sh.row0 == 0 ? static_cast<void *>(sh.table[t & 1].p) : static_cast<void *>(sh.intro_buf.p);
+        GSP_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, 0, s->comm, s->st));
+        s->perf.xgmi_bytes += sh.row0 == 0 ? double(bytes) * double(s->shards - 1) : 0.0;
+        return GSP_OK;
+    }
+    const Shard &root = s->local[0];
+    for (Shard &sh : s->local)
+        if (sh.row0 != 0) {
+            GSP_HIP(hipMemcpyAsync(sh.intro_buf.p, root.table[t & 1].p, bytes, hipMemcpyDeviceToDevice, s->st));
+            s->perf.xgmi_bytes += double(bytes);
+        }
+    return GSP_OK;
+}
+
+// the delivered JOINREPs of tick t into every local shard's receiver CSR (after the scan)
+int join_scatter(gsp_scale *s, int32_t t) {
+    const int64_t cnt = s->plan.count(t);
+    if (!s->joins || cnt == 0) return GSP_OK;
+    for (Shard &sh : s->local)
+        GSP_HIP(gsp::launch_join_scatter(sh.joiners.p + s->plan.first(t), sh.join_ok.p + s->plan.first(t),
+                                         int32_t(cnt), s->rowmode ? sh.row0 : 0,
+                                         s->rowmode ? sh.rows : s->p.n, sh.off.p, sh.fill.p, sh.csr_src.p,
+                                         s->rowmode ? sh.x.csr_slot.p : nullptr, s->st));
+    return GSP_OK;
+}
+
 int collect_timing(gsp_scale *s) {
     for (auto &t : s->pending) {
         float a = 0.f, b = 0.f;
@@ -396,6 +470,9 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                                        int64_t(double(rows_max) * p->fanout / shards * 1.25) + 4096);
     }
     s->h_fail = gsp::scale_fail_ticks(*p);
+    s->h_start = gsp::start_ticks(p->policy, p->n);
+    s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
+    if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
     if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 7;
     if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
     if (!s->sliced) {
@@ -432,6 +509,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
         if (int rc = resolve_sends(s.get(), 0)) return rc;
     if (s->rowmode)
         if (int rc = exchange_row_counts(s.get(), 0)) return rc;
+    if (int rc = join_sends(s.get(), 0)) return rc;
     GSP_HIP(hipStreamSynchronize(s->st));
     *out = s.release();
     return GSP_OK;
@@ -521,6 +599,7 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
                 GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
             }
         }
+        if (int rc = join_scatter(s, t)) return rc;
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (Shard &sh : s->local)
             GSP_HIP(gsp::launch_scale_tick(s->args(sh, t), s->sliced, s->merge, s->st));
@@ -532,6 +611,7 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
             if (int rc = resolve_sends(s, t)) return rc;
         if (s->rowmode)
             if (int rc = exchange_row_counts(s, t)) return rc;
+        if (int rc = join_sends(s, t)) return rc;
         s->tick = t;
         s->perf.ticks++;
     }

@@ -12,6 +12,7 @@
 // One 256-lane workgroup per row streams the row in 2048-column chunks: it reads its own
 // row and each sender's row once (16 B per lane, fully coalesced) and writes its row once,
 // so the kernel is HBM-bound at (2 + k) * stride * 2 bytes per row with k messages.
+#include "join_kernels.hpp"
 #include "philox.hpp"
 #include "scale_kernels.hpp"
 #include "wave_ops.hpp"
@@ -169,17 +170,73 @@ __device__ inline uint32_t wave_excl_prefix(uint32_t v, int32_t, uint32_t *total
     return incl - v;
 }
 
-// Sequential sampling without replacement: draw k maps u % (cnt - k) onto the ranks not
-// chosen yet, in ascending order (chosen[] kept sorted).  Identical in every lane.
-__device__ inline int32_t next_distinct_rank(uint32_t u, int32_t cnt, int32_t k, int32_t *chosen,
-                                             int32_t &nch) {
-    int32_t rk = int32_t(u % uint32_t(cnt - k));
-    int32_t pos = 0;
-    while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
-    for (int32_t q = nch; q > pos; --q) chosen[q] = chosen[q - 1];
-    chosen[pos] = rk;
-    nch++;
-    return rk;
+// JOINREP payload (the bounded introducer list, join_kernels.hpp): the B = min(intro_list,
+// cnt0) ranks Philox(JOIN; t - 1, 0, r, i) chooses among node 0's cnt0 gossipable members of
+// tick t - 1, resolved to this slice's columns by one forward pass of wave 0 over the
+// introducer's row (512 columns per step: a ballot-free wave prefix of the step's member
+// counts).  Writes the chosen (global column, entry) pairs this slice holds to jc / jv and
+// returns their number (wave 0 only; every lane gets the same result).
+__device__ inline int32_t join_choose(const ScaleTickArgs &a, int32_t r, int32_t t, int32_t *jc,
+                                      uint32_t *jv) {
+    const int32_t lane = threadIdx.x & 63;
+    const int32_t cnt0 = a.cnt_prev[0];
+    const int32_t B = a.intro_list < cnt0 ? a.intro_list : cnt0;
+    int32_t ranks[kMaxIntro];
+    int32_t nch = 0;
+    for (int32_t i = 0; i < B; ++i)
+        next_distinct_rank(draw_u31(kDomainJoin, a.seed, uint32_t(t - 1), 0u, uint32_t(r), uint32_t(i)),
+                           cnt0, i, ranks, nch);
+    int32_t pre = 0, own = cnt0;          // ranks [pre, pre + own) live in this slice
+    if (a.intro_cnt) {
+        own = a.intro_cnt[int64_t(a.shard) * a.n];
+        for (int32_t g = 0; g < a.shard; ++g) pre += a.intro_cnt[int64_t(g) * a.n];
+    }
+    const uint32_t tf = uint32_t(a.tfail), t5m1 = uint32_t(t - 1) & 31u;
+    int32_t q = 0, found = 0;
+    while (q < B && ranks[q] < pre) ++q;
+    int32_t seen = pre;                   // gossipable members before the current step
+    for (int64_t c0 = 0; c0 < a.stride && q < B && ranks[q] < pre + own; c0 += 512) {
+        const int64_t c = c0 + int64_t(lane) * 8;
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (c < a.stride) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(a.intro + c);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        }
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const uint32_t ent = (w[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+            const bool g = ent && (tf == 0 || ((t5m1 - ent) & 31u) < tf);
+            bits |= (g ? 1u : 0u) << e;
+        }
+        const uint32_t cnt = __builtin_popcount(bits);
+        const uint32_t incl = wave_incl_scan(cnt);
+        const int32_t total = int32_t(lane_of(incl, 63));
+        while (q < B && ranks[q] < seen + total) {
+            const uint32_t want = uint32_t(ranks[q] - seen);          // rank within the step
+            const bool mine = want >= incl - cnt && want < incl;
+            const unsigned long long who = __ballot(mine);
+            const int32_t l = __builtin_ffsll(who) - 1;
+            uint32_t col = 0, val = 0;
+            if (mine) {
+                uint32_t m = want - (incl - cnt), bb = bits;
+                for (uint32_t z = 0; z < m; ++z) bb &= bb - 1;
+                const int e = __builtin_ffs(bb) - 1;
+                col = uint32_t(c) + uint32_t(e);
+                val = (w[e >> 1] >> ((e & 1) * 16)) & 0xFFFFu;
+            }
+            col = lane_of(col, l);
+            val = lane_of(val, l);
+            if (found < kMaxIntro) {
+                jc[found] = int32_t(int64_t(a.col0) + col);
+                jv[found] = val;
+            }
+            found++;
+            q++;
+        }
+        seen += total;
+    }
+    return found;
 }
 
 // kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads.
@@ -198,6 +255,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     __shared__ int32_t s_src[kMaxSegment];
     __shared__ int32_t s_slot[kMaxSegment];
     __shared__ unsigned long long s_red[4][4];
+    __shared__ int32_t s_jc[kMaxIntro];      // JOINREP payload: chosen columns / entries
+    __shared__ uint32_t s_jv[kMaxIntro];
+    __shared__ int32_t s_njc;
 
     const int32_t tid = threadIdx.x;
     const int32_t lane = tid & 63, wave = tid >> 6;
@@ -207,7 +267,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     const int32_t F = a.fanout;
 
     if (!kInit && *a.err) return;      // a capacity error froze the job at an earlier tick
-    if (t > a.fail_tick[r]) {          // crashed (Application.cpp:186): no recv, no ops, no send
+    // crashed (Application.cpp:186) or not started yet (Application.cpp:143): no recv, no
+    // ops, no send
+    if (t > a.fail_tick[r] || (a.start_tick && t < a.start_tick[r])) {
         if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
         return;
     }
@@ -244,6 +306,17 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             if (rank[q] >= 0) { s_src[rank[q]] = val[q]; s_slot[rank[q]] = slot[q]; }
         __syncthreads();
     }
+    // a JOINREP (sender kJoinRepSrc, sorted first) is merged apart from the GOSSIP loop: wave 0
+    // resolves its payload columns, and the GOSSIPs are s_src[jr .. k)
+    const int32_t jr = (!kInit && k > 0 && s_src[0] == kJoinRepSrc) ? 1 : 0;
+    if (jr) {
+        if (wave == 0) {
+            const int32_t nj = join_choose(a, r, t, s_jc, s_jv);
+            if (lane == 0) s_njc = nj < kMaxIntro ? nj : kMaxIntro;
+        }
+        __syncthreads();
+    }
+    const int32_t njc = jr ? s_njc : 0;
 
     const uint32_t t5 = uint32_t(t) & 31u;
     const uint32_t tr = uint32_t(a.tremove);
@@ -268,9 +341,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             for (int32_t i = 0; i < a.swim; ++i) {
                 const uint32_t dr = draw_u31(kDomainPing, a.seed, uint32_t(t - 1), uint32_t(r),
                                              uint32_t(pcol), uint32_t(i));
-                ok = ok || int32_t(dr % 100u) >= a.drop_pct;
+                ok = ok || int32_t(dr % 100u) >= a.drop_prev;     // paths sent at t - 1
             }
-            ok = ok && t <= a.fail_tick[pcol];
+            ok = ok && t <= a.fail_tick[pcol] && (!a.start_tick || t >= a.start_tick[pcol]);
             pts = ok ? t5 : ((t5 - tr) & 31u);
         }
     }
@@ -288,13 +361,13 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         pe = ld16<kNtOwn>(own_prev + col);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (u < k) pv[u] = ld16<kNtSrc>(srow[u] + col);
+            if (jr + u < k) pv[u] = ld16<kNtSrc>(srow[u] + col);
     };
     if (kPipe && !kInit) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             pv[u] = make_uint4(0u, 0u, 0u, 0u);
-            const int32_t sl = __builtin_amdgcn_readfirstlane(u < k ? s_slot[u] : 0);
+            const int32_t sl = __builtin_amdgcn_readfirstlane(jr + u < k ? s_slot[jr + u] : 0);
             srow[u] = sl >= 0 ? a.prev + int64_t(sl) * stride : a.remote + int64_t(-sl - 1) * stride;
         }
         issue(int64_t(tid) * kEntriesPerLane);
@@ -306,13 +379,18 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         uint32_t ws[4];
         uint32_t w0[4] = {0u, 0u, 0u, 0u};
         if (kInit) {
+            // pre-joined: the nodes that start at tick 0 list each other (h0, ts 0)
+            const bool late_row = a.start_tick && a.start_tick[r] > 0;
             const uint32_t h = uint32_t(a.h0) << 5;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const int64_t x0 = gc0 + 2 * i, x1 = x0 + 1;
-                const uint32_t lo = (x0 < a.n && x0 != r) ? h : 0u;
-                const uint32_t hi = (x1 < a.n && x1 != r) ? h : 0u;
-                ws[i] = lo | (hi << 16);
+                bool on0 = x0 < a.n && x0 != r && !late_row, on1 = x1 < a.n && x1 != r && !late_row;
+                if (a.start_tick) {
+                    on0 = on0 && a.start_tick[x0] == 0;
+                    on1 = on1 && a.start_tick[x1] == 0;
+                }
+                ws[i] = (on0 ? h : 0u) | ((on1 ? h : 0u) << 16);
             }
         } else {
             uint4 e;
@@ -328,9 +406,21 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                 e = ld16<kNtOwn>(own_prev + lc0);
             }
             w0[0] = e.x; w0[1] = e.y; w0[2] = e.z; w0[3] = e.w;
-            for (int32_t j0 = 0; j0 < k; j0 += 4) {
+            if (jr) {                         // the JOINREP: the introducer's sender entry
+                const int64_t d0 = -gc0;      // (MP1Node.cpp:237-243), then its chosen members
+                if (d0 >= 0 && d0 < kEntriesPerLane)
+                    patch16(e, int(d0), [t5](uint32_t old) { return old ? ((((old >> 5) + 1u) << 5) | t5)
+                                                                        : ((1u << 5) | t5); });
+                for (int32_t q = 0; q < njc; ++q) {
+                    const int64_t dq = int64_t(s_jc[q]) - gc0;
+                    const uint32_t v = s_jv[q];
+                    if (dq >= 0 && dq < kEntriesPerLane)
+                        patch16(e, int(dq), [v, t5, tr](uint32_t old) { return merge_entry(old, v, t5, tr); });
+                }
+            }
+            for (int32_t j0 = jr; j0 < k; j0 += 4) {
                 uint4 v[4];
-                if (kPipe && j0 == 0) {
+                if (kPipe && j0 == jr) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) v[u] = cv[u];
                 } else {
@@ -443,7 +533,11 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             a.own_hb[lr] += 1;
             if (a.count_rounds) {
                 unsigned long long merges = 0;
-                for (int32_t j = 0; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
+                if (jr) {                     // a JOINREP carries min(B, cnt0) members
+                    const int32_t c0 = a.cnt_prev[0];
+                    merges += 1ull + uint64_t(a.intro_list < c0 ? a.intro_list : c0);
+                }
+                for (int32_t j = jr; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
                 atomicAdd(&dig[kDigRounds], 1ull);
                 atomicAdd(&dig[kDigMerges], merges);
                 atomicAdd(&dig[kDigDelivered], (unsigned long long)k);
@@ -510,7 +604,7 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
     if (s >= a.n) return;
     const int32_t F = a.fanout;
     const int32_t W = F + (a.swim > 0 ? 1 : 0);        // pick slots per sender
-    if (a.tick > a.fail_tick[s]) {
+    if (a.tick > a.fail_tick[s] || (a.start_tick && a.tick < a.start_tick[s])) {
         if (lane < W) a.picks[int64_t(s) * W + lane] = -1;
         return;
     }

@@ -48,6 +48,15 @@ struct ScaleTickArgs {
     int32_t count_rounds;        // this shard adds node-rounds / merges / sends to the digest
     uint64_t seed;
     const int32_t *fail_tick;    // [n] global
+    const int32_t *start_tick;   // [n] global, or null: every node starts at tick 0 (policy.hpp)
+    int32_t drop_prev;           // drop percentage of the sends of tick - 1 (SWIM probe paths)
+    // JOINREPs (join_kernels.hpp): a receiver whose segment starts with kJoinRepSrc merges the
+    // introducer's row of tick - 1 cut to intro_list Philox-chosen gossipable members
+    const uint16_t *intro;       // node 0's row of tick - 1, this table's columns
+    int32_t intro_list;          // B (gsp_policy.intro_list)
+    const int32_t *intro_cnt;    // column shards: cnt_all ([shards][n]: node 0's slice counts at
+                                 // intro_cnt[g * n]); null: one slice holds the whole row
+    int32_t shards, shard;       // column shards: this slice's index among `shards`
     int32_t *own_hb;             // [rows]
     const int32_t *cnt_prev;     // [n] member counts at t-1 (global ids)
     int32_t *cnt_cur;            // [n] (fused: member count; slice: count in this slice)
@@ -75,6 +84,7 @@ hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipS
 //   finalize (after an all-reduce MAX of picks): drop draw, out_dst, deg.
 struct ScaleResolveArgs {
     int32_t n, fanout, tick, drop_pct, shard, shards, count_rounds;
+    const int32_t *start_tick;   // [n] or null
     int32_t swim;                // SWIM probing: picks hold fanout + 1 slots per sender, the
                                  // last one the probe target; finalize copies it to ping[]
     int64_t stride;              // slice width

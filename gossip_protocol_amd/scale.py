@@ -9,7 +9,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, lib
 
-FAIL_NONE, FAIL_RANDOM, FAIL_BLOCK = 0, 1, 2
+FAIL_NONE, FAIL_RANDOM, FAIL_BLOCK, FAIL_SINGLE, FAIL_HALF = 0, 1, 2, 3, 4
+make_policy = _lib.make_policy
 LAYOUTS = {"columns": 0, "rows": 1}
 
 
@@ -17,6 +18,15 @@ def unpack(entries):
     e = np.asarray(entries, dtype=np.uint16)
     present = e != 0
     return present, (e >> 5).astype(np.int32), (e & 31).astype(np.int32)
+
+
+def params_from_conf(path):
+    """gsp_scale_params from a .conf (the reference's four keys, then optional scale keys;
+    include/gossip/gossip.h gsp_scale_params_from_conf)."""
+    p = _lib.GspScaleParams()
+    check(lib().gsp_scale_params_from_conf(path.encode(), ctypes.byref(p)),
+          "gsp_scale_params_from_conf")
+    return p
 
 
 def nccl_unique_id():
@@ -41,11 +51,16 @@ class ScaleEngine:
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
                  fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0, group=1,
-                 rank=0, world=1, nccl_id=None, layout="columns", tfail=0, swim=0):
-        self.params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
-                                          h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
-                                          fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks,
-                                          tfail=tfail, swim=swim)
+                 rank=0, world=1, nccl_id=None, layout="columns", tfail=0, swim=0, policy=None,
+                 events=False, event_cap=0, params=None):
+        if params is None:
+            params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
+                                         h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
+                                         fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks,
+                                         tfail=tfail, swim=swim, policy=policy or _lib.GspPolicy(),
+                                         events=int(events), event_cap=event_cap)
+        self.params = params
+        n, fanout = params.n, params.fanout
         self._h = ctypes.c_void_p()
         lay = LAYOUTS[layout]
         if nccl_id is not None:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 2
+#define GSP_ABI_VERSION 3
 
 typedef enum {
     GSP_OK = 0,
@@ -59,6 +59,8 @@ int gsp_device_count(void);
 #define GSP_DOMAIN_SEND 0x53454E44u
 #define GSP_DOMAIN_FAIL 0x4641494Cu
 #define GSP_DOMAIN_PEER 0x50454552u
+#define GSP_DOMAIN_PING 0x50494E47u
+#define GSP_DOMAIN_JOIN 0x4A4F494Eu
 uint32_t gsp_replay_draw(uint32_t domain, uint64_t seed, uint32_t a, uint32_t b, uint32_t c,
                          uint32_t d);
 int gsp_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
@@ -184,6 +186,47 @@ typedef struct {
 int gsp_exact_stats_get(gsp_engine *e, gsp_exact_stats *out);
 
 /* ------------------------------------------------------------------------------------
+ * Driver policies of the scale engines.  The reference hard-codes them in
+ * its driver -- node i starts at tick (int)(STEP_RATE * i) (Application.cpp:143,
+ * Params.cpp:30), messages are dropped in the window t in [50, 300) (Application.cpp:177,
+ * 198), one random node or N/2 contiguous nodes crash at t = 100 (Application.cpp:180-196);
+ * the scale engines take them as data, run on the device.  All zeros = the pre-joined,
+ * always-dropping, single-event protocol of ABI 2.
+ * ---------------------------------------------------------------------------------- */
+#define GSP_MAX_FAIL_EVENTS 8
+typedef enum {
+    GSP_FAIL_NONE = 0,
+    GSP_FAIL_RANDOM = 1,   /* each node with probability ppm / 10^6                        */
+    GSP_FAIL_BLOCK = 2,    /* n * ppm / 10^6 contiguous nodes from a Philox start (wrapping) */
+    GSP_FAIL_SINGLE = 3,   /* one node: Philox % n (Application.cpp:182)                    */
+    GSP_FAIL_HALF = 4      /* n / 2 contiguous nodes from (Philox % n) / 2 (Application.cpp:189) */
+} gsp_fail_mode;
+typedef struct {
+    int32_t tick;          /* the nodes crash at the end of this tick                       */
+    int32_t mode;          /* gsp_fail_mode                                                 */
+    int32_t ppm;           /* fraction for RANDOM / BLOCK, parts per million                */
+} gsp_fail_event;
+typedef struct {
+    int32_t drop_from, drop_until;  /* drop_pct applies to the sends of ticks t with
+                                       drop_from <= t < drop_until (drop_until <= 0: no end) */
+    double step_rate;               /* join schedule: node i starts at tick (int)(step_rate * i);
+                                       0: every node pre-joined.  Nodes starting at 0 list each
+                                       other; a later node starts with an empty list and, one
+                                       tick before, node 0 (the introducer, MP1Node.cpp:378-386)
+                                       sends it a JOINREP if alive (drop draw Philox(SEND; t, 0,
+                                       j, JOINREP)).  The JOINREP merges like a GOSSIP from node
+                                       0 whose payload is the bounded introducer list below.   */
+    int32_t intro_list;             /* JOINREP payload bound B (0..16): B members of node 0's
+                                       gossipable list, Philox-chosen (Philox(JOIN; t, 0, j, i)
+                                       sequential distinct ranks) -- MP1Node.cpp:221-230 sends
+                                       the whole list and its receiver ignores it (:231-233)   */
+    int32_t n_fail_events;          /* further crash events, applied after the one of
+                                       (fail_mode, fail_tick, fail_ppm); event e draws with
+                                       index e + 1                                           */
+    gsp_fail_event fail_events[GSP_MAX_FAIL_EVENTS];
+} gsp_policy;
+
+/* ------------------------------------------------------------------------------------
  * SCALE engine (full view, packed entries, device-resident tick loop)
  * ---------------------------------------------------------------------------------- */
 typedef struct gsp_scale gsp_scale;
@@ -208,6 +251,11 @@ typedef struct {
                            s - 1 indirect paths; answered -> ts refreshed, unanswered ->
                            removed at the next tick (DESIGN.md "Scale mode"); every
                            layout                                                      */
+    gsp_policy policy;  /* join schedule + bounded introducer list, drop window, crash
+                           events (all zero: off)                                      */
+    int32_t events;     /* 1: keep every join / remove event in a device ring, drained with
+                           gsp_scale_drain_events (Log.cpp:116-130's lines at scale)     */
+    int64_t event_cap;  /* ring capacity in events (0: 2^24)                            */
 } gsp_scale_params;
 
 typedef struct {
@@ -224,6 +272,19 @@ typedef struct {
     double xgmi_bytes;        /* bytes this engine's shards sent to other shards, summed
                                  over ticks (0 on one GPU)                              */
 } gsp_scale_perf;
+
+/* Scale parameters from a .conf: the reference's four keys exactly as Params::setparams reads
+ * them (Params.cpp:22-25; every reference testcase parses unchanged) mapped as its driver uses
+ * them -- n = MAX_NNB, SINGLE_FAILURE 1: one Philox-chosen node crashes at t = 100, 0: n/2
+ * contiguous nodes (Application.cpp:180-196), DROP_MSG: drop_pct = (int)(MSG_DROP_PROB * 100)
+ * in [50, 300) (EmulNet.cpp:91, Application.cpp:177/198), STEP_RATE 0.25, 700 ticks -- then
+ * optional "KEY: value" lines: SCALE_N FANOUT TREMOVE TFAIL SWIM H0 SEED TICKS STEP_RATE
+ * INTRO_LIST DROP_PCT DROP_WINDOW(from until) FAIL(tick mode ppm, repeatable) EVENTS EVENT_CAP,
+ * and for the partial view VIEW INBOX.  Unknown keys fail with GSP_ERR_INVALID. */
+int gsp_scale_params_from_conf(const char *path, gsp_scale_params *out);
+/* sizeof of a public struct by name ("gsp_scale_params", ...; 0 if unknown): lets a binding
+ * check its layout */
+int64_t gsp_struct_size(const char *name);
 
 /* Single-GPU engine on `device` (rows [0, n), full rows, fused tick kernel). */
 int gsp_scale_create(const gsp_scale_params *p, int device, gsp_scale **out);
@@ -302,6 +363,10 @@ typedef struct {
     int32_t n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm;
     uint64_t seed;
     int32_t max_ticks;
+    int32_t tfail, swim;  /* as gsp_scale_params: TFAIL suspicion, SWIM probing (0: off)   */
+    gsp_policy policy;    /* as gsp_scale_params                                         */
+    int32_t events;       /* 1: keep every join / remove / evict event (gsp_pview_drain_events) */
+    int64_t event_cap;    /* ring capacity in events (0: 2^24)                            */
 } gsp_pview_params;
 
 typedef struct {
@@ -311,6 +376,8 @@ typedef struct {
                               2 remove, 3 evict */
 } gsp_pview_digest;
 
+/* As gsp_scale_params_from_conf, plus the VIEW / INBOX keys (defaults 256 / 7). */
+int gsp_pview_params_from_conf(const char *path, gsp_pview_params *out);
 int gsp_pview_create(const gsp_pview_params *p, int device, gsp_pview **out);
 /* Row-sharded job (DESIGN.md "Partial view, row shards").  Shard g of G owns the views of
  * nodes [floor(g n / G), floor((g + 1) n / G)); per tick every sender view that a message

@@ -35,6 +35,32 @@ int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int t
                        const char *dbg_path, const char *msgcount_path, const char *state_path,
                        const char *stdout_path);
 
+/* ---- driver policies shared by both scale restatements (schedule.c) ----
+ * The reference hard-codes them in its driver (Application.cpp:143, 177-200; Params.cpp:30);
+ * the scale protocols take them as data.  Same layout as gsp_policy in include/gossip/gossip.h. */
+#define GSP_ORACLE_MAX_FAIL_EVENTS 8
+typedef struct { int32_t tick, mode, ppm; } gsp_oracle_fail_event;
+enum { GSP_OFAIL_NONE = 0, GSP_OFAIL_RANDOM = 1, GSP_OFAIL_BLOCK = 2, GSP_OFAIL_SINGLE = 3,
+       GSP_OFAIL_HALF = 4 };
+typedef struct {
+    int32_t drop_from, drop_until;  /* drop_pct applies to sends at ticks t, from <= t < until
+                                       (until <= 0: no end); Application.cpp:177, 198      */
+    double step_rate;               /* join schedule: node i starts at tick (int)(step_rate i)
+                                       (Application.cpp:143, Params.cpp:30); 0: pre-joined  */
+    int32_t intro_list;             /* JOINREP payload bound B, 0..16 (MP1Node.cpp:221-230)  */
+    int32_t n_fail_events;          /* further failure events (index e + 1 in the draws)    */
+    gsp_oracle_fail_event fail_events[GSP_ORACLE_MAX_FAIL_EVENTS];
+} gsp_oracle_policy;
+/* start ticks / crash ticks of every node, and the drop percentage of sends at tick t */
+void gsp_sched_start_ticks(const gsp_oracle_policy *p, int32_t n, int32_t *start);
+void gsp_sched_fail_ticks(const gsp_oracle_policy *p, int32_t n, uint64_t seed, int32_t mode0,
+                          int32_t tick0, int32_t ppm0, int32_t *fail);
+int32_t gsp_sched_drop(const gsp_oracle_policy *p, int32_t drop_pct, int32_t t);
+/* the B_eff = min(B, cnt) distinct ranks a JOINREP sent at tick t to joiner j carries, among
+ * the introducer's cnt gossipable members (ascending); returns B_eff */
+int32_t gsp_sched_intro_ranks(const gsp_oracle_policy *p, uint64_t seed, int32_t t, int32_t j,
+                              int32_t cnt, int32_t *ranks);
+
 /* ---- scale protocol restatement (scale_oracle.c) ---- */
 typedef struct {
     int32_t n;          /* nodes (full view: V = n)                         */
@@ -51,6 +77,7 @@ typedef struct {
                            peers, not counted (MP1Node.h:22, spec p.3)         */
     int32_t swim;       /* 0: off; s >= 1: SWIM ping/ack probing with one direct path
                            and s - 1 indirect (ping-req) paths (spec p.3)      */
+    gsp_oracle_policy pol; /* drop window, join schedule + JOINREP bound, failure events */
 } gsp_scale_cfg;
 
 typedef struct {
@@ -75,9 +102,16 @@ int gsp_scale_oracle_row(const gsp_scale_oracle *o, int32_t r, uint8_t *present,
                          int32_t *ts);
 int gsp_scale_oracle_own_hb(const gsp_scale_oracle *o, int32_t r);
 int32_t gsp_scale_oracle_fail_tick(const gsp_scale_oracle *o, int32_t r);
-/* The messages (src, dst) sent at the last completed tick that survived the drop draw. */
+/* The GOSSIP messages (src, dst) sent at the last completed tick that survived the drop
+ * draw; the JOINREPs (node 0 -> joiner) separately; start / crash tick of a node. */
 int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32_t *dst,
                                   int64_t cap);
+int64_t gsp_scale_oracle_joinreps(const gsp_scale_oracle *o, int32_t *dst, int64_t cap);
+int32_t gsp_scale_oracle_start_tick(const gsp_scale_oracle *o, int32_t r);
+/* The join (kind 1) / remove (kind 2) events of the last step (row r, member x), rows
+ * ascending, a row's joins before its removes, members ascending. */
+int64_t gsp_scale_oracle_events(const gsp_scale_oracle *o, int32_t *kind, int32_t *r, int32_t *x,
+                                int64_t cap);
 
 /* The scale protocol's per-row rules (the reference's, MP1Node.cpp:237-251, 282-301, 339-348),
  * exported so tests can feed them the reference's own rows: one GOSSIP merge, and the
@@ -104,6 +138,8 @@ typedef struct {
     int32_t inbox;      /* K: messages merged per node per tick (rest = overflow)   */
     int32_t drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm;
     uint64_t seed;
+    int32_t tfail, swim;   /* as gsp_scale_cfg */
+    gsp_oracle_policy pol;
 } gsp_pview_cfg;
 
 typedef struct {
@@ -123,6 +159,11 @@ int gsp_pview_oracle_own_hb(const gsp_pview_oracle *o, int32_t r);
 int32_t gsp_pview_oracle_fail_tick(const gsp_pview_oracle *o, int32_t r);
 int64_t gsp_pview_oracle_messages(const gsp_pview_oracle *o, int32_t *src, int32_t *dst,
                                   int64_t cap);
+int64_t gsp_pview_oracle_joinreps(const gsp_pview_oracle *o, int32_t *dst, int64_t cap);
+int32_t gsp_pview_oracle_start_tick(const gsp_pview_oracle *o, int32_t r);
+/* join (1) / remove (2) / evict (3) events of the last step */
+int64_t gsp_pview_oracle_events(const gsp_pview_oracle *o, int32_t *kind, int32_t *r, int32_t *x,
+                                int64_t cap);
 /* The per-row rule of gsp_pview_oracle_step for ONE alive row r at tick t, on views the caller
  * hands in (ids ascending, absolute ts): own view, the ids that sent to r at t - 1 (any order
  * and count: sorted, the first `inbox` merged, the rest counted as overflow) and their views

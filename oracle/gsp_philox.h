@@ -21,6 +21,7 @@
 #define GSP_DOMAIN_FAIL 0x4641494Cu /* "FAIL": failure-injection draw     */
 #define GSP_DOMAIN_PEER 0x50454552u /* "PEER": scale-mode peer choice     */
 #define GSP_DOMAIN_PING 0x50494E47u /* "PING": SWIM probe target / paths  */
+#define GSP_DOMAIN_JOIN 0x4A4F494Eu /* "JOIN": bounded introducer list     */
 
 static inline void gsp_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2],
                                      uint32_t out[4]) {

@@ -13,6 +13,16 @@
  * filters ids >= 10, MP1Node.cpp:245) is fixed by the build: pre-joined start, no id
  * filter, receipt in ascending sender order, Philox peer choice (fanout f, distinct
  * peers) and Philox drop/failure draws.
+ * Driver policies (schedule.c; the reference's Application.cpp:143, 177-200 as data): a node
+ * is alive from its start tick to its crash tick; sends are dropped only inside the drop
+ * window.  Nodes starting at tick 0 are pre-joined (they list each other).  A later node j
+ * starts with an empty list; at tick start_j - 1 the introducer (node 0, MP1Node.cpp:378-386),
+ * if alive, sends it a JOINREP (drop draw: Philox(SEND; t, 0, j, 1), msgType JOINREP) whose
+ * payload is a bounded introducer list -- intro_list members of the introducer's gossipable
+ * list chosen by Philox (gsp_sched_intro_ranks; MP1Node.cpp:221-230 sends the whole list, and
+ * its receiver ignores it, :231-233).  The receiver handles a JOINREP like a GOSSIP from
+ * node 0 with that payload: the introducer enters as (1, t), the chosen members are copied if
+ * fresh.  It is always node 0's only message that tick, so it merges first.
  * TFAIL suspicion (the reference defines TFAIL = 5, MP1Node.h:22, and never
  * uses it): with cfg.tfail > 0 a member whose heartbeat is tfail or more ticks old is
  * SUSPECTED -- still listed until TREMOVE, but left out of the payload a node gossips, of its
@@ -25,11 +35,13 @@
  * gossip peers.  The probe (ping + ack, one round trip) is resolved in r's tick t + 1, after
  * r's gossip merges and before its TREMOVE scan: it is answered iff p is alive at t + 1 and
  * at least one of s paths survives its drop draw (Philox(PING; t, r, p, i) % 100 >=
- * drop_pct, i = 0 direct, 1..s-1 indirect ping-req relays).  Answered: r refreshes p's
+ * drop(t), i = 0 direct, 1..s-1 indirect ping-req relays).  Answered: r refreshes p's
  * timestamp (ts = t + 1, hb unchanged, so hb <= h0 + t still holds).  Unanswered: r declares
  * p failed -- ts = (t + 1) - TREMOVE, so the scan of the same tick removes it (one remove
  * event).  The probe target was listed when chosen and merges never remove, so it is listed
  * at resolution time.
+ * Every join / remove event of the last step is kept (gsp_scale_oracle_events) for the
+ * device event stream's parity tests.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -37,16 +49,20 @@
 #include "gsp_oracle.h"
 #include "gsp_philox.h"
 
+enum { MSG_JOINREP = 1, MSG_GOSSIP = 3 };
+
 struct gsp_scale_oracle {
     gsp_scale_cfg c;
     int32_t t;
     int cur;
     uint8_t *pres[2];
     int32_t *hb[2], *ts[2];
-    int32_t *own_hb, *fail_tick, *cnt;
+    int32_t *own_hb, *fail_tick, *start_tick, *cnt;
     int32_t *ping;                  /* swim: probe target of each node's last send, or -1 */
-    int32_t *msrc, *mdst;
+    int32_t *msrc, *mdst, *mtype;   /* messages of the last send phase (GOSSIP and JOINREP) */
     int64_t nmsg, mcap;
+    int32_t *ev_kind, *ev_r, *ev_x; /* events of the last step */
+    int64_t nev, evcap;
 };
 
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
@@ -58,33 +74,56 @@ uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
     return z ^ (z >> 31);
 }
 
-static int alive_at(const gsp_scale_oracle *o, int32_t r, int32_t t) { return t <= o->fail_tick[r]; }
+static int alive_at(const gsp_scale_oracle *o, int32_t r, int32_t t) {
+    return o->start_tick[r] <= t && t <= o->fail_tick[r];
+}
 
 /* a listed member with timestamp ts is gossiped / chosen / counted at tick t */
 static int gossipable(const gsp_scale_cfg *c, int32_t t, int32_t ts) {
     return c->tfail <= 0 || t - ts < c->tfail;
 }
 
-static void compute_fail_ticks(gsp_scale_oracle *o) {
-    const gsp_scale_cfg *c = &o->c;
-    for (int32_t r = 0; r < c->n; ++r) o->fail_tick[r] = 0x7FFFFFFF;
-    if (c->fail_mode == 1) {
-        for (int32_t r = 0; r < c->n; ++r)
-            if (gsp_philox_u31(GSP_DOMAIN_FAIL, c->seed, (uint32_t)c->fail_tick, (uint32_t)r, 0, 0) %
-                    1000000u < (uint32_t)c->fail_ppm)
-                o->fail_tick[r] = c->fail_tick;
-    } else if (c->fail_mode == 2) {
-        int64_t m = (int64_t)c->n * c->fail_ppm / 1000000;
-        uint32_t start = gsp_philox_u31(GSP_DOMAIN_FAIL, c->seed, (uint32_t)c->fail_tick,
-                                        0xFFFFFFFFu, 0, 0) % (uint32_t)c->n;
-        for (int64_t i = 0; i < m; ++i) o->fail_tick[(start + i) % c->n] = c->fail_tick;
+static void push_msg(gsp_scale_oracle *o, int32_t s, int32_t d, int32_t type) {
+    if (o->nmsg == o->mcap) {
+        o->mcap = o->mcap ? o->mcap * 2 : 1024;
+        o->msrc = realloc(o->msrc, sizeof(int32_t) * o->mcap);
+        o->mdst = realloc(o->mdst, sizeof(int32_t) * o->mcap);
+        o->mtype = realloc(o->mtype, sizeof(int32_t) * o->mcap);
     }
+    o->msrc[o->nmsg] = s;
+    o->mdst[o->nmsg] = d;
+    o->mtype[o->nmsg] = type;
+    o->nmsg++;
 }
 
-/* Phase SEND of tick t for every alive node, reading table `tab`. */
+static void push_event(gsp_scale_oracle *o, int32_t kind, int32_t r, int32_t x) {
+    if (o->nev == o->evcap) {
+        o->evcap = o->evcap ? o->evcap * 2 : 1024;
+        o->ev_kind = realloc(o->ev_kind, sizeof(int32_t) * o->evcap);
+        o->ev_r = realloc(o->ev_r, sizeof(int32_t) * o->evcap);
+        o->ev_x = realloc(o->ev_x, sizeof(int32_t) * o->evcap);
+    }
+    o->ev_kind[o->nev] = kind;
+    o->ev_r[o->nev] = r;
+    o->ev_x[o->nev] = x;
+    o->nev++;
+}
+
+/* rank -> column: the rk-th gossipable column of row (ps, tss) at tick t, ascending */
+static int32_t column_of_rank(const gsp_scale_cfg *c, const uint8_t *ps, const int32_t *tss,
+                              int32_t t, int32_t rk) {
+    int32_t seen = -1;
+    for (int32_t x = 0; x < c->n; ++x)
+        if (ps[x] && gossipable(c, t, tss[x]) && ++seen == rk) return x;
+    return -1;
+}
+
+/* Phase SEND of tick t for every alive node, reading table `tab`; then the JOINREPs the
+ * introducer sends at t to the nodes that start at t + 1. */
 static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d) {
     const gsp_scale_cfg *c = &o->c;
     const int32_t n = c->n;
+    const int32_t drop = gsp_sched_drop(&c->pol, c->drop_pct, t);
     o->nmsg = 0;
     int32_t chosen[64];
     for (int32_t s = 0; s < n; ++s) {
@@ -103,37 +142,86 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
             memmove(&chosen[pos + 1], &chosen[pos], sizeof(int32_t) * (nch - pos));
             chosen[pos] = rk;
             nch++;
-            /* rank -> column: rk-th gossipable column in ascending order */
-            int32_t seen = -1, dst = -1;
-            for (int32_t x = 0; x < n; ++x)
-                if (ps[x] && gossipable(c, t, tss[x]) && ++seen == rk) { dst = x; break; }
+            int32_t dst = column_of_rank(c, ps, tss, t, rk);
             if (d) d->sent++;
             uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, (uint32_t)s,
                                          (uint32_t)dst, 3u);
-            if ((int32_t)(dr % 100u) < c->drop_pct) {
+            if ((int32_t)(dr % 100u) < drop) {
                 if (d) d->dropped++;
                 continue;
             }
-            if (o->nmsg == o->mcap) {
-                o->mcap = o->mcap ? o->mcap * 2 : 1024;
-                o->msrc = realloc(o->msrc, sizeof(int32_t) * o->mcap);
-                o->mdst = realloc(o->mdst, sizeof(int32_t) * o->mcap);
-            }
-            o->msrc[o->nmsg] = s;
-            o->mdst[o->nmsg] = dst;
-            o->nmsg++;
+            push_msg(o, s, dst, MSG_GOSSIP);
         }
         if (c->swim > 0) {      /* the probe target: one more rank-select over the same order */
             o->ping[s] = -1;
             if (cnt > 0) {
                 int32_t rk = (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)t,
                                                       (uint32_t)s, 0, 0x100) % (uint32_t)cnt);
-                int32_t seen = -1;
-                for (int32_t x = 0; x < n; ++x)
-                    if (ps[x] && gossipable(c, t, tss[x]) && ++seen == rk) { o->ping[s] = x; break; }
+                o->ping[s] = column_of_rank(c, ps, tss, t, rk);
             }
         }
     }
+    if (!alive_at(o, 0, t)) return;             /* JOINREPs to the nodes starting at t + 1 */
+    for (int32_t j = 1; j < n; ++j) {
+        if (o->start_tick[j] != t + 1) continue;
+        if (d) d->sent++;
+        uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, 0, (uint32_t)j, 1u);
+        if ((int32_t)(dr % 100u) < drop) {
+            if (d) d->dropped++;
+            continue;
+        }
+        push_msg(o, 0, j, MSG_JOINREP);
+    }
+}
+
+gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg) {
+    if (!cfg || cfg->n < 2 || cfg->fanout < 1 || cfg->fanout > 60 ||
+        cfg->swim < 0 || cfg->swim > 8 || cfg->pol.intro_list < 0 || cfg->pol.intro_list > 16)
+        return NULL;
+    gsp_scale_oracle *o = calloc(1, sizeof *o);
+    o->c = *cfg;
+    const int32_t n = cfg->n;
+    size_t nn = (size_t)n * n;
+    for (int b = 0; b < 2; ++b) {
+        o->pres[b] = calloc(nn, 1);
+        o->hb[b] = calloc(nn, sizeof(int32_t));
+        o->ts[b] = calloc(nn, sizeof(int32_t));
+    }
+    o->own_hb = calloc(n, sizeof(int32_t));
+    o->fail_tick = calloc(n, sizeof(int32_t));
+    o->start_tick = calloc(n, sizeof(int32_t));
+    o->cnt = calloc(n, sizeof(int32_t));
+    o->ping = malloc(sizeof(int32_t) * n);
+    for (int32_t r = 0; r < n; ++r) o->ping[r] = -1;
+    gsp_sched_start_ticks(&cfg->pol, n, o->start_tick);
+    gsp_sched_fail_ticks(&cfg->pol, n, cfg->seed, cfg->fail_mode, cfg->fail_tick, cfg->fail_ppm,
+                         o->fail_tick);
+    /* tick 0: the nodes that start at 0 are pre-joined: each lists the others with (h0, 0) */
+    for (int32_t r = 0; r < n; ++r) {
+        int32_t cnt = 0;
+        for (int32_t x = 0; x < n; ++x) {
+            size_t i = (size_t)r * n + x;
+            const int on = x != r && o->start_tick[r] == 0 && o->start_tick[x] == 0;
+            o->pres[0][i] = (uint8_t)on;
+            o->hb[0][i] = on ? cfg->h0 : 0;
+            o->ts[0][i] = 0;
+            cnt += on;
+        }
+        o->cnt[r] = cnt;
+    }
+    o->cur = 0;
+    o->t = 0;
+    send_all(o, 0, 0, NULL);
+    return o;
+}
+
+void gsp_scale_oracle_destroy(gsp_scale_oracle *o) {
+    if (!o) return;
+    for (int b = 0; b < 2; ++b) { free(o->pres[b]); free(o->hb[b]); free(o->ts[b]); }
+    free(o->own_hb); free(o->fail_tick); free(o->start_tick); free(o->cnt);
+    free(o->msrc); free(o->mdst); free(o->mtype); free(o->ping);
+    free(o->ev_kind); free(o->ev_r); free(o->ev_x);
+    free(o);
 }
 
 /* ---- the per-row rules, exported (tests/test_scale_rules_vs_reference.py feeds them the
@@ -184,48 +272,6 @@ int32_t gsp_scale_oracle_remove_scan(int32_t n, int32_t t, int32_t T, int32_t tf
     return live;
 }
 
-gsp_scale_oracle *gsp_scale_oracle_create(const gsp_scale_cfg *cfg) {
-    if (!cfg || cfg->n < 2 || cfg->fanout < 1 || cfg->fanout > 60 ||
-        cfg->swim < 0 || cfg->swim > 8) return NULL;
-    gsp_scale_oracle *o = calloc(1, sizeof *o);
-    o->c = *cfg;
-    const int32_t n = cfg->n;
-    size_t nn = (size_t)n * n;
-    for (int b = 0; b < 2; ++b) {
-        o->pres[b] = calloc(nn, 1);
-        o->hb[b] = calloc(nn, sizeof(int32_t));
-        o->ts[b] = calloc(nn, sizeof(int32_t));
-    }
-    o->own_hb = calloc(n, sizeof(int32_t));
-    o->fail_tick = calloc(n, sizeof(int32_t));
-    o->cnt = calloc(n, sizeof(int32_t));
-    o->ping = malloc(sizeof(int32_t) * n);
-    for (int32_t r = 0; r < n; ++r) o->ping[r] = -1;
-    compute_fail_ticks(o);
-    /* tick 0: pre-joined, every other node present with (h0, 0) */
-    for (int32_t r = 0; r < n; ++r) {
-        for (int32_t x = 0; x < n; ++x) {
-            size_t i = (size_t)r * n + x;
-            o->pres[0][i] = (x != r);
-            o->hb[0][i] = (x != r) ? cfg->h0 : 0;
-            o->ts[0][i] = 0;
-        }
-        o->cnt[r] = n - 1;
-    }
-    o->cur = 0;
-    o->t = 0;
-    send_all(o, 0, 0, NULL);
-    return o;
-}
-
-void gsp_scale_oracle_destroy(gsp_scale_oracle *o) {
-    if (!o) return;
-    for (int b = 0; b < 2; ++b) { free(o->pres[b]); free(o->hb[b]); free(o->ts[b]); }
-    free(o->own_hb); free(o->fail_tick); free(o->cnt); free(o->msrc); free(o->mdst);
-    free(o->ping);
-    free(o);
-}
-
 int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
     const gsp_scale_cfg *c = &o->c;
     const int32_t n = c->n, T = c->tremove;
@@ -233,8 +279,10 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
     const int prev = o->cur, next = 1 - o->cur;
     memset(d, 0, sizeof *d);
     d->tick = t;
+    o->nev = 0;
 
-    /* bucket last tick's surviving messages by destination, ascending sender */
+    /* bucket last tick's surviving messages by destination, ascending sender (message index
+     * carried along; a JOINREP comes from node 0, which sends no GOSSIP to a joiner) */
     int32_t *deg = calloc((size_t)n + 1, sizeof(int32_t));
     for (int64_t m = 0; m < o->nmsg; ++m) deg[o->mdst[m] + 1]++;
     for (int32_t r = 0; r < n; ++r) deg[r + 1] += deg[r];
@@ -242,19 +290,21 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
     int32_t *bucket = malloc(sizeof(int32_t) * (o->nmsg ? o->nmsg : 1));
     for (int64_t m = 0; m < o->nmsg; ++m) {
         int32_t r = o->mdst[m];
-        bucket[deg[r] + fill[r]++] = o->msrc[m];
+        bucket[deg[r] + fill[r]++] = (int32_t)m;
     }
-    for (int32_t r = 0; r < n; ++r) { /* insertion sort each (tiny) bucket */
+    for (int32_t r = 0; r < n; ++r) { /* insertion sort each (tiny) bucket by sender */
         int32_t *b = bucket + deg[r];
         int32_t k = deg[r + 1] - deg[r];
         for (int32_t i = 1; i < k; ++i) {
             int32_t v = b[i], j = i - 1;
-            while (j >= 0 && b[j] > v) { b[j + 1] = b[j]; j--; }
+            while (j >= 0 && o->msrc[b[j]] > o->msrc[v]) { b[j + 1] = b[j]; j--; }
             b[j + 1] = v;
         }
     }
 
     int32_t *cnt_next = malloc(sizeof(int32_t) * n);
+    uint8_t *Pj = malloc((size_t)n), *P0 = malloc((size_t)n);
+    int32_t ranks[16];
     for (int32_t r = 0; r < n; ++r) {
         const size_t row = (size_t)r * n;
         uint8_t *P = o->pres[next] + row;
@@ -264,29 +314,51 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
         memcpy(S, o->ts[prev] + row, sizeof(int32_t) * n);
         if (!alive_at(o, r, t)) { cnt_next[r] = o->cnt[r]; continue; }
         d->node_rounds++;
+        memcpy(P0, P, n);
         for (int32_t j = deg[r]; j < deg[r + 1]; ++j) {
-            const int32_t s = bucket[j];
+            const int32_t m = bucket[j], s = o->msrc[m];
             const size_t srow = (size_t)s * n;
             const uint8_t *Ps = o->pres[prev] + srow;
             const int32_t *Hs = o->hb[prev] + srow, *Ss = o->ts[prev] + srow;
             d->delivered++;
-            d->merges += 1 + o->cnt[s];
-            /* the payload: s's members gossipable when s sent it (tick t - 1) */
-            gsp_scale_oracle_merge_msg(n, t, T, c->tfail, r, P, H, S, s, Ps, Hs, Ss, &d->joins,
-                                       &d->event_hash);
+            if (o->mtype[m] == MSG_JOINREP) {
+                /* the bounded introducer list: the chosen ranks among node 0's gossipable
+                 * members of tick t - 1 */
+                const int32_t b = gsp_sched_intro_ranks(&c->pol, c->seed, t - 1, r, o->cnt[0], ranks);
+                memset(Pj, 0, (size_t)n);
+                for (int32_t i = 0; i < b; ++i) {
+                    const int32_t x = column_of_rank(c, Ps, Ss, t - 1, ranks[i]);
+                    if (x >= 0) Pj[x] = 1;
+                }
+                d->merges += 1 + b;
+                gsp_scale_oracle_merge_msg(n, t, T, 0, r, P, H, S, s, Pj, Hs, Ss, &d->joins,
+                                           &d->event_hash);
+            } else {
+                d->merges += 1 + o->cnt[s];
+                /* the payload: s's members gossipable when s sent it (tick t - 1) */
+                gsp_scale_oracle_merge_msg(n, t, T, c->tfail, r, P, H, S, s, Ps, Hs, Ss,
+                                           &d->joins, &d->event_hash);
+            }
         }
         if (c->swim > 0 && o->ping[r] >= 0) {   /* resolve the probe sent at t - 1 */
             const int32_t p = o->ping[r];
+            const int32_t drop = gsp_sched_drop(&c->pol, c->drop_pct, t - 1);
             int ok = 0;
             for (int32_t i = 0; i < c->swim; ++i)
                 ok |= (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)(t - 1), (uint32_t)r,
-                                               (uint32_t)p, (uint32_t)i) % 100u) >= c->drop_pct;
+                                               (uint32_t)p, (uint32_t)i) % 100u) >= drop;
             if (P[p]) S[p] = (ok && alive_at(o, p, t)) ? t : t - T;
         }
         o->own_hb[r] += 1;
+        for (int32_t x = 0; x < n; ++x)         /* the row's join events, then its removes */
+            if (P[x] && !P0[x]) push_event(o, 1, r, x);
+        for (int32_t x = 0; x < n; ++x)
+            if (P[x] && t - S[x] >= T) push_event(o, 2, r, x);
         cnt_next[r] = gsp_scale_oracle_remove_scan(n, t, T, c->tfail, r, P, H, S, &d->removes,
                                                    &d->event_hash);
     }
+    free(Pj);
+    free(P0);
     memcpy(o->cnt, cnt_next, sizeof(int32_t) * n);
     free(cnt_next); free(deg); free(fill); free(bucket);
     o->cur = next;
@@ -307,13 +379,43 @@ int gsp_scale_oracle_row(const gsp_scale_oracle *o, int32_t r, uint8_t *present,
 
 int gsp_scale_oracle_own_hb(const gsp_scale_oracle *o, int32_t r) { return o->own_hb[r]; }
 int32_t gsp_scale_oracle_fail_tick(const gsp_scale_oracle *o, int32_t r) { return o->fail_tick[r]; }
+int32_t gsp_scale_oracle_start_tick(const gsp_scale_oracle *o, int32_t r) { return o->start_tick[r]; }
 
+/* GOSSIP messages of the last send phase: (src, dst) pairs; JOINREPs are not listed */
 int64_t gsp_scale_oracle_messages(const gsp_scale_oracle *o, int32_t *src, int32_t *dst,
                                   int64_t cap) {
-    int64_t k = o->nmsg < cap ? o->nmsg : cap;
-    if (src) memcpy(src, o->msrc, sizeof(int32_t) * k);
-    if (dst) memcpy(dst, o->mdst, sizeof(int32_t) * k);
-    return o->nmsg;
+    int64_t k = 0;
+    for (int64_t m = 0; m < o->nmsg; ++m) {
+        if (o->mtype[m] != MSG_GOSSIP) continue;
+        if (k < cap) {
+            if (src) src[k] = o->msrc[m];
+            if (dst) dst[k] = o->mdst[m];
+        }
+        k++;
+    }
+    return k;
+}
+
+/* The JOINREPs of the last send phase (their destinations, ascending). */
+int64_t gsp_scale_oracle_joinreps(const gsp_scale_oracle *o, int32_t *dst, int64_t cap) {
+    int64_t k = 0;
+    for (int64_t m = 0; m < o->nmsg; ++m)
+        if (o->mtype[m] == MSG_JOINREP) {
+            if (dst && k < cap) dst[k] = o->mdst[m];
+            k++;
+        }
+    return k;
+}
+
+/* The join (kind 1) / remove (kind 2) events of the last step, rows ascending, joins of a
+ * row before its removes, members ascending. */
+int64_t gsp_scale_oracle_events(const gsp_scale_oracle *o, int32_t *kind, int32_t *r, int32_t *x,
+                                int64_t cap) {
+    const int64_t k = o->nev < cap ? o->nev : cap;
+    if (kind) memcpy(kind, o->ev_kind, sizeof(int32_t) * (size_t)k);
+    if (r) memcpy(r, o->ev_r, sizeof(int32_t) * (size_t)k);
+    if (x) memcpy(x, o->ev_x, sizeof(int32_t) * (size_t)k);
+    return o->nev;
 }
 
 /* exported for the known-answer tests */

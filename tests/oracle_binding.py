@@ -16,11 +16,39 @@ MODES = ["glibc", "philox"]
 FILES = ["dbg.log", "msgcount.log", "state.txt", "stdout.txt"]
 
 
+MAX_FAIL_EVENTS = 8
+
+
+class FailEvent(ctypes.Structure):
+    _fields_ = [("tick", ctypes.c_int32), ("mode", ctypes.c_int32), ("ppm", ctypes.c_int32)]
+
+
+class Policy(ctypes.Structure):
+    """gsp_oracle_policy (oracle/gsp_oracle.h) == gsp_policy (include/gossip/gossip.h)."""
+    _fields_ = [("drop_from", ctypes.c_int32), ("drop_until", ctypes.c_int32),
+                ("step_rate", ctypes.c_double), ("intro_list", ctypes.c_int32),
+                ("n_fail_events", ctypes.c_int32), ("fail_events", FailEvent * MAX_FAIL_EVENTS)]
+
+
+def make_policy(drop_window=None, step_rate=0.0, intro_list=0, fail_events=()):
+    """drop_window=(from, until); fail_events=[(tick, mode, ppm), ...]."""
+    p = Policy()
+    if drop_window:
+        p.drop_from, p.drop_until = drop_window
+    p.step_rate = step_rate
+    p.intro_list = intro_list
+    p.n_fail_events = len(fail_events)
+    for i, (tk, md, pp) in enumerate(fail_events):
+        p.fail_events[i] = FailEvent(tk, md, pp)
+    return p
+
+
 class ScaleCfg(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("fanout", ctypes.c_int32), ("drop_pct", ctypes.c_int32),
                 ("tremove", ctypes.c_int32), ("h0", ctypes.c_int32), ("fail_mode", ctypes.c_int32),
                 ("fail_tick", ctypes.c_int32), ("fail_ppm", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32), ("swim", ctypes.c_int32)]
+                ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32), ("swim", ctypes.c_int32),
+                ("pol", Policy)]
 
 
 class TickDigest(ctypes.Structure):
@@ -39,7 +67,8 @@ class PviewCfg(ctypes.Structure):
                 ("inbox", ctypes.c_int32), ("drop_pct", ctypes.c_int32),
                 ("tremove", ctypes.c_int32), ("h0", ctypes.c_int32), ("fail_mode", ctypes.c_int32),
                 ("fail_tick", ctypes.c_int32), ("fail_ppm", ctypes.c_int32),
-                ("seed", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32), ("swim", ctypes.c_int32),
+                ("pol", Policy)]
 
 
 class PviewDigest(ctypes.Structure):
@@ -80,6 +109,16 @@ def load_oracle():
         L.gsp_scale_oracle_own_hb.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.gsp_scale_oracle_fail_tick.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.gsp_scale_oracle_fail_tick.restype = ctypes.c_int32
+        for pre in ("gsp_scale_oracle", "gsp_pview_oracle"):
+            f = getattr(L, pre + "_start_tick")
+            f.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+            f.restype = ctypes.c_int32
+            f = getattr(L, pre + "_joinreps")
+            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
+            f.restype = ctypes.c_int64
+            f = getattr(L, pre + "_events")
+            f.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int64]
+            f.restype = ctypes.c_int64
         L.gsp_scale_oracle_messages.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_int64]
         L.gsp_scale_oracle_messages.restype = ctypes.c_int64
@@ -171,12 +210,33 @@ def run_oracle_mp1(conf, seed, mode, out_dir, ticks=700):
 
 class ScaleOracle:
     """The scale-protocol restatement (oracle/scale_oracle.c)."""
+    _pre = "gsp_scale_oracle"
+
+    def start_tick(self, r):
+        return getattr(self.L, self._pre + "_start_tick")(self.h, r)
+
+    def joinreps(self):
+        import numpy as np
+        f = getattr(self.L, self._pre + "_joinreps")
+        n = f(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        f(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def events(self):
+        """(kind, r, x) arrays of the last step's events."""
+        import numpy as np
+        f = getattr(self.L, self._pre + "_events")
+        n = f(self.h, None, None, None, 0)
+        k, r, x = (np.zeros(max(n, 1), np.int32) for _ in range(3))
+        f(self.h, k.ctypes.data, r.ctypes.data, x.ctypes.data, n)
+        return k[:n], r[:n], x[:n]
 
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=0, fail_tick=10,
-                 fail_ppm=0, seed=0x5EED, tfail=0, swim=0):
+                 fail_ppm=0, seed=0x5EED, tfail=0, swim=0, policy=None):
         self.L = load_oracle()
         self.cfg = ScaleCfg(n, fanout, drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm, seed,
-                            tfail, swim)
+                            tfail, swim, policy or Policy())
         self.h = self.L.gsp_scale_oracle_create(ctypes.byref(self.cfg))
         assert self.h, "oracle create failed"
         self.n = n
@@ -248,12 +308,33 @@ def pview_row_step(cfg, t, r, own, senders, views):
 
 class PviewOracle:
     """The partial-view restatement (oracle/pview_oracle.c)."""
+    _pre = "gsp_pview_oracle"
+
+    def start_tick(self, r):
+        return getattr(self.L, self._pre + "_start_tick")(self.h, r)
+
+    def joinreps(self):
+        import numpy as np
+        f = getattr(self.L, self._pre + "_joinreps")
+        n = f(self.h, None, 0)
+        out = np.zeros(max(n, 1), np.int32)
+        f(self.h, out.ctypes.data, n)
+        return out[:n]
+
+    def events(self):
+        """(kind, r, x) arrays of the last step's events."""
+        import numpy as np
+        f = getattr(self.L, self._pre + "_events")
+        n = f(self.h, None, None, None, 0)
+        k, r, x = (np.zeros(max(n, 1), np.int32) for _ in range(3))
+        f(self.h, k.ctypes.data, r.ctypes.data, x.ctypes.data, n)
+        return k[:n], r[:n], x[:n]
 
     def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
-                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED):
+                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, tfail=0, swim=0, policy=None):
         self.L = load_oracle()
         self.cfg = PviewCfg(n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick,
-                            fail_ppm, seed)
+                            fail_ppm, seed, tfail, swim, policy or Policy())
         self.h = self.L.gsp_pview_oracle_create(ctypes.byref(self.cfg))
         assert self.h, "pview oracle create failed"
         self.n, self.view = n, view

@@ -109,3 +109,60 @@ def test_scale_variant_params_validated_before_the_device():
         for ok in (dict(swim=8), dict(tfail=5, swim=1)):
             sp = _lib.GspScaleParams(**base, **ok)
             assert L.gsp_scale_create(ctypes.byref(sp), 0, ctypes.byref(h)) not in (0, -1), ok
+
+
+def test_struct_layouts_match_the_header():
+    """Every public struct the ctypes stub mirrors has the C ABI's size."""
+    L = _lib.lib()
+    for name, cls in [("gsp_params", _lib.GspParams), ("gsp_member_view", _lib.GspMemberView),
+                      ("gsp_entry", _lib.GspEntry), ("gsp_exact_stats", _lib.GspExactStats),
+                      ("gsp_fail_event", _lib.GspFailEvent), ("gsp_policy", _lib.GspPolicy),
+                      ("gsp_scale_params", _lib.GspScaleParams),
+                      ("gsp_scale_digest", _lib.GspScaleDigest),
+                      ("gsp_scale_perf", _lib.GspScalePerf),
+                      ("gsp_pview_params", _lib.GspPviewParams),
+                      ("gsp_pview_digest", _lib.GspPviewDigest)]:
+        assert L.gsp_struct_size(name.encode()) == ctypes.sizeof(cls), name
+    assert L.gsp_abi_version() == 3
+
+
+def test_scale_params_from_reference_conf():
+    """The reference's own testcases parse unchanged (Params.cpp:22-25's four keys) into the
+    scale protocol the way its driver uses them (Application.cpp:143, 177-200)."""
+    from gossip_protocol_amd.scale import FAIL_HALF, FAIL_SINGLE, params_from_conf
+    for conf, mode, drop in [("singlefailure", FAIL_SINGLE, 0), ("multifailure", FAIL_HALF, 0),
+                             ("msgdropsinglefailure", FAIL_SINGLE, 10)]:
+        p = params_from_conf(os.path.join(GOLDEN, "testcases", conf + ".conf"))
+        assert (p.n, p.fail_mode, p.fail_tick, p.drop_pct) == (10, mode, 100, drop)
+        assert p.policy.step_rate == 0.25 and p.max_ticks == 700 and p.tremove == 20
+        assert (p.policy.drop_from, p.policy.drop_until) == ((50, 300) if drop else (0, 0))
+        assert p.policy.intro_list == 0 and p.policy.n_fail_events == 0
+
+
+def test_scale_params_extended_keys(tmp_path):
+    from gossip_protocol_amd.pview import params_from_conf as pv_conf
+    from gossip_protocol_amd.scale import FAIL_BLOCK, FAIL_RANDOM, params_from_conf
+    path = str(tmp_path / "x.conf")
+    with open(path, "w") as f:
+        f.write("MAX_NNB: 10\nSINGLE_FAILURE: 1\nDROP_MSG: 1\nMSG_DROP_PROB: 0.2\n"
+                "SCALE_N: 4096\nFANOUT: 5\nSEED: 77\nTICKS: 64\nSTEP_RATE: 0.01\n"
+                "INTRO_LIST: 8\nDROP_WINDOW: 3 30\nFAIL: 20 RANDOM 10000\nFAIL: 25 BLOCK 50000\n"
+                "FAIL: 40 3 0\nTFAIL: 5\nSWIM: 2\nEVENTS: 1\n\n")
+    p = params_from_conf(path)
+    assert (p.n, p.fanout, p.seed, p.max_ticks, p.drop_pct) == (4096, 5, 77, 64, 20)
+    assert (p.fail_tick, p.fail_mode, p.fail_ppm) == (20, FAIL_RANDOM, 10000)
+    assert p.policy.n_fail_events == 2
+    assert (p.policy.fail_events[0].tick, p.policy.fail_events[0].mode) == (25, FAIL_BLOCK)
+    assert (p.policy.drop_from, p.policy.drop_until, p.policy.intro_list) == (3, 30, 8)
+    assert abs(p.policy.step_rate - 0.01) < 1e-12 and (p.tfail, p.swim, p.events) == (5, 2, 1)
+    with open(path, "a") as f:
+        f.write("VIEW: 64\nINBOX: 5\n")
+    q = pv_conf(path)
+    assert (q.n, q.view, q.inbox, q.fanout, q.tfail, q.swim) == (4096, 64, 5, 5, 5, 2)
+    L = _lib.lib()
+    assert L.gsp_scale_params_from_conf(path.encode(), ctypes.byref(_lib.GspScaleParams())) == -1
+    assert b"partial-view" in L.gsp_last_error()
+    with open(path, "a") as f:
+        f.write("BOGUS: 1\n")
+    assert L.gsp_pview_params_from_conf(path.encode(), ctypes.byref(_lib.GspPviewParams())) == -1
+    assert b"unknown key BOGUS" in L.gsp_last_error()
