@@ -184,11 +184,48 @@ SIGNATURES = {
     "gsp_pview_own_hb": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
     "gsp_pview_messages": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int64, P(c_int64)]),
     "gsp_pview_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
+    "gsp_scale_drain_events": (ctypes.c_int, [ctypes.c_void_p, P(c_uint64), c_int64, P(c_int64),
+                                              P(c_int64)]),
+    "gsp_pview_drain_events": (ctypes.c_int, [ctypes.c_void_p, P(c_uint64), c_int64, P(c_int64),
+                                              P(c_int64)]),
+    "gsp_events_write_log": (ctypes.c_int, [P(c_uint64), c_int64, ctypes.c_char_p]),
 }
 
 
 class GspError(RuntimeError):
     pass
+
+
+EVENT_JOIN, EVENT_REMOVE, EVENT_EVICT = 1, 2, 3
+
+
+def drain_events(fn, handle):
+    """Drain an engine's event ring (gsp_scale_drain_events / gsp_pview_drain_events):
+    (records as uint64 numpy array, lost count)."""
+    import numpy as np
+    n, lost = ctypes.c_int64(), ctypes.c_int64()
+    check(fn(handle, None, 0, ctypes.byref(n), ctypes.byref(lost)), "drain_events")
+    buf = np.zeros(max(n.value, 1), np.uint64)
+    check(fn(handle, buf.ctypes.data_as(P(c_uint64)), n.value, ctypes.byref(n), ctypes.byref(lost)),
+          "drain_events")
+    return buf[:n.value], lost.value
+
+
+def split_events(rec):
+    """(kind, tick, r, x) arrays of event records."""
+    import numpy as np
+    rec = np.asarray(rec, np.uint64)
+    return ((rec >> np.uint64(62)).astype(np.int32), ((rec >> np.uint64(42)) & np.uint64(0xFFFFF)).astype(np.int32),
+            ((rec >> np.uint64(21)) & np.uint64(0x1FFFFF)).astype(np.int32),
+            (rec & np.uint64(0x1FFFFF)).astype(np.int32))
+
+
+def write_event_log(rec, path):
+    """gsp_events_write_log: the records as dbg.log lines (sorted canonically)."""
+    import numpy as np
+    rec = np.ascontiguousarray(rec, np.uint64).copy()
+    check(lib().gsp_events_write_log(rec.ctypes.data_as(P(c_uint64)), len(rec), path.encode()),
+          "gsp_events_write_log")
 
 
 _lib = None

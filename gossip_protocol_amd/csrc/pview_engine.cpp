@@ -40,7 +40,7 @@ struct PvShard {
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok;
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
-    gsp::DevBuf<unsigned long long> dig, prof, rowdig;
+    gsp::DevBuf<unsigned long long> dig, prof, rowdig, ev_buf, ev_count;
     gsp::RowxBufs x;             // row exchange (G > 1)
 
     void release() {
@@ -54,6 +54,8 @@ struct PvShard {
         dig.release();
         prof.release();
         rowdig.release();
+        ev_buf.release();
+        ev_count.release();
     }
 };
 
@@ -73,6 +75,7 @@ struct gsp_pview {
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
+    int64_t ev_cap = 0;          // event ring capacity per shard (events on)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail, h_start;
@@ -135,6 +138,9 @@ struct gsp_pview {
         a.order = sort_rows ? sh.order.p : nullptr;
         a.prof = sh.prof.p;
         a.waves = waves;
+        a.ev_buf = p.events ? sh.ev_buf.p : nullptr;
+        a.ev_count = sh.ev_count.p;
+        a.ev_cap = ev_cap;
         return a;
     }
 
@@ -235,6 +241,11 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
         // a late joiner's (empty) view is read at its start tick from either buffer
         GSP_HIP(hipMemsetAsync(sh.table[1].p, 0xFF, rows * size_t(V) * 8, st));
         if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(V)));
+    }
+    if (s->p.events) {
+        GSP_HIP(sh.ev_buf.alloc(size_t(s->ev_cap)));
+        GSP_HIP(sh.ev_count.alloc(1));
+        GSP_HIP(hipMemsetAsync(sh.ev_count.p, 0, 8, st));
     }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
@@ -362,6 +373,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
+    s->ev_cap = p->events ? (p->event_cap > 0 ? p->event_cap : (int64_t(1) << 24)) : 0;
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
@@ -574,6 +586,30 @@ int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n) {
         total += slots;
     }
     *n = total;
+    return GSP_OK;
+}
+
+// Same contract as gsp_scale_drain_events (gossip.h): the join / remove / evict records of every
+// tick since the last drain, shard by shard, in device append order.
+int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost) {
+    GSP_REQUIRE(s && n && cap >= 0 && (buf || cap == 0), GSP_ERR_INVALID, "gsp_pview_drain_events: bad argument");
+    GSP_REQUIRE(s->p.events, GSP_ERR_INVALID, "gsp_pview_drain_events: the engine records no events "
+                "(gsp_pview_params.events = 0)");
+    if (int rc = gsp_pview_sync(s)) return rc;
+    int64_t total = 0, dropped = 0;
+    for (PvShard &sh : s->local) {
+        unsigned long long c = 0;
+        GSP_HIP(hipMemcpy(&c, sh.ev_count.p, 8, hipMemcpyDeviceToHost));
+        const int64_t have = std::min<int64_t>(int64_t(c), s->ev_cap);
+        dropped += int64_t(c) - have;
+        if (buf && total < cap && have > 0)
+            GSP_HIP(hipMemcpy(buf + total, sh.ev_buf.p, size_t(std::min(have, cap - total)) * 8,
+                              hipMemcpyDeviceToHost));
+        total += have;
+        if (buf) GSP_HIP(hipMemset(sh.ev_count.p, 0, 8));
+    }
+    *n = total;
+    if (lost) *lost = dropped;
     return GSP_OK;
 }
 

@@ -29,6 +29,7 @@
 #include "join_kernels.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
+#include "scale_kernels.hpp"
 #include "wave_ops.hpp"
 
 namespace gsp {
@@ -245,13 +246,30 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         for (int32_t i = 0; i < nch; ++i) chosen = chosen || (g && uint32_t(ranks[i]) == rank);
         if (!chosen) ent[1] = kPvEmpty;
     }
+    // A TFAIL- or introducer-filtered payload has holes: its keys are compacted to the front
+    // of the block (the tree merges sorted blocks).  Block-uniform; one scan per message.
+    int32_t kpos[kBlocks];                               // slot of this lane's key
+    uint32_t kpad = 0;                                   // bit m: lane pads its own slot of block m
+#pragma unroll
+    for (int m = 0; m < kBlocks; ++m) {
+        kpos[m] = tid;
+        if (m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
+            const bool ok = ent[m] != kPvEmpty;
+            uint32_t cnt = 0;
+            const uint32_t pos = block_scan(ok ? 1u : 0u, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
+            kpos[m] = ok ? int32_t(pos) : -1;
+            kpad |= uint32_t(tid >= int32_t(cnt)) << m;
+        }
+    }
     uint32_t merged = 0;                                 // payload entries (MP1Node.cpp:245 trips)
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
         const bool ok = ent[m] != kPvEmpty;
         merged += (m >= 1 && ok) ? 1u : 0u;
-        sh.keys[0][m * kSlots + tid] =
-            ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
+        if ((kpad >> m) & 1u) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted block's tail
+        if (kpos[m] >= 0)
+            sh.keys[0][m * kSlots + kpos[m]] =
+                ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
         sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
         if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
     }
@@ -326,6 +344,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
 
     uint32_t res[Q], rid[Q];
     uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
+    uint32_t jmask = 0, rmask = 0;                       // event stream: join / remove keys
     uint64_t hsum = 0;
     // the run being folded: id, value, own-view value, sender event (message index, applied)
     uint32_t ax = kNoId, av = 0, ae0 = 0, ajs = 0;
@@ -372,10 +391,11 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (ajs && !adone) av = pv_event(av, t5);
         if (x == uint32_t(r) || !av) continue;                  // never list yourself
         if (x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
-        if (!ae0) { joins++; hsum += pv_hash(S_join, x); }
+        if (!ae0) { joins++; hsum += pv_hash(S_join, x); jmask |= 1u << e; }
         if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
             hsum += pv_hash(S_remove, x);
+            rmask |= 1u << e;
             continue;
         }
         res[e] = av;
@@ -401,6 +421,21 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
     }
 
+    if (a.ev_buf) {                                      // event stream: joins and removes
+        uint64_t p = wave_reserve_events(a.ev_count, uint32_t(__popc(jmask) + __popc(rmask) + __popc(adopt)));
+        auto put = [&](uint32_t kind, uint32_t x) {
+            if (int64_t(p) < a.ev_cap) a.ev_buf[p] = event_record(kind, t, uint32_t(r), x);
+            ++p;
+        };
+#pragma unroll
+        for (int e = 0; e < Q; ++e) {
+            if ((jmask >> e) & 1u) put(1u, key_id(ck[e]));
+            if ((rmask >> e) & 1u) put(2u, key_id(ck[e]));
+        }
+#pragma unroll
+        for (int jj = 0; jj < kJ; ++jj)
+            if ((adopt >> jj) & 1u) put(1u, ssrc[jj]);
+    }
     pm.mark(3);
     // ---- 5a. survivors (and adopted orphans), compacted in id order -------------------------
     // for_each visits this lane's survivors in id order as (value, id)
@@ -549,6 +584,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
+        uint64_t evp = 0;                                  // event stream: this lane's evictions
+        if (a.ev_buf) {
+            const int32_t tk = int32_t(need2) - int32_t(tie_before);
+            const uint32_t kept = nk + uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
+            evp = wave_reserve_events(a.ev_count, nloc - kept);
+        }
         for_each([&](uint32_t v, uint32_t x, uint32_t b) {
             const uint32_t hb = v >> 5;
             bool keep = b < bstar || (b == bstar && (!tie || hb > hstar));
@@ -560,6 +601,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             } else {
                 evicts++;
                 hsum += pv_hash(S_evict, x);
+                if (a.ev_buf) {
+                    if (int64_t(evp) < a.ev_cap) a.ev_buf[evp] = event_record(3u, t, uint32_t(r), x);
+                    ++evp;
+                }
             }
         });
         ro.ids_off = lds_word(sh, Wid);

@@ -39,7 +39,7 @@ struct Shard {
         ping, deg, off, fill, csr_src, err, tile_sum, start_tick, joiners, join_ok;
     gsp::DevBuf<uint16_t> intro_buf;   // row layout, shards != 0: node 0's row of the last tick
     gsp::DevBuf<uint8_t> bitmap;
-    gsp::DevBuf<unsigned long long> dig;
+    gsp::DevBuf<unsigned long long> dig, ev_buf, ev_count;
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
@@ -49,6 +49,8 @@ struct Shard {
         intro_buf.release();
         bitmap.release();
         dig.release();
+        ev_buf.release();
+        ev_count.release();
         x.release();
     }
 };
@@ -68,6 +70,7 @@ struct gsp_scale {
     int32_t *h_err = nullptr;  // pinned mirror of the shards' capacity flags, refreshed by an
                                // async copy at the end of every gsp_scale_step call
     int32_t max_segment = gsp::kMaxSegment;
+    int64_t ev_cap = 0;        // event ring capacity per shard (events on)
     ncclComm_t comm = nullptr; // one shard per process when set
     int64_t width = 0;         // n rounded up to 2048 * G
     int64_t stride = 0;        // columns per shard
@@ -140,6 +143,9 @@ struct gsp_scale {
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
         a.max_segment = max_segment;
+        a.ev_buf = p.events ? sh.ev_buf.p : nullptr;
+        a.ev_count = sh.ev_count.p;
+        a.ev_cap = ev_cap;
         return a;
     }
 
@@ -237,6 +243,11 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(sh.dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
+    if (s->p.events) {
+        GSP_HIP(sh.ev_buf.alloc(size_t(s->ev_cap)));
+        GSP_HIP(sh.ev_count.alloc(1));
+        GSP_HIP(hipMemsetAsync(sh.ev_count.p, 0, 8, st));
+    }
     if (s->joins) {
         GSP_HIP(sh.start_tick.alloc(size_t(n)));
         GSP_HIP(hipMemcpyAsync(sh.start_tick.p, s->h_start.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
@@ -246,8 +257,9 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
         if (!s->plan.joiners.empty())
             GSP_HIP(hipMemcpyAsync(sh.joiners.p, s->plan.joiners.data(), s->plan.joiners.size() * 4,
                                    hipMemcpyHostToDevice, st));
-        // a late joiner's row is read (empty) at its start tick from either buffer
-        GSP_HIP(hipMemsetAsync(sh.table[1].p, 0, tab * sizeof(uint16_t), st));
+        // a late joiner's row is read (empty) at its start tick from either buffer, and the
+        // init kernel skips the rows that have not started
+        for (int b = 0; b < 2; ++b) GSP_HIP(hipMemsetAsync(sh.table[b].p, 0, tab * sizeof(uint16_t), st));
         if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(s->stride)));
     }
     GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
@@ -470,6 +482,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                                        int64_t(double(rows_max) * p->fanout / shards * 1.25) + 4096);
     }
     s->h_fail = gsp::scale_fail_ticks(*p);
+    s->ev_cap = p->events ? (p->event_cap > 0 ? p->event_cap : (int64_t(1) << 24)) : 0;
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
@@ -764,6 +777,28 @@ int gsp_scale_layout(gsp_scale *s, int32_t *shards, int32_t *rank, int64_t *stri
     if (shards) *shards = s->shards;
     if (rank) *rank = s->rank;
     if (stride) *stride = s->stride;
+    return GSP_OK;
+}
+
+int gsp_scale_drain_events(gsp_scale *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost) {
+    GSP_REQUIRE(s && n && cap >= 0 && (buf || cap == 0), GSP_ERR_INVALID, "gsp_scale_drain_events: bad argument");
+    GSP_REQUIRE(s->p.events, GSP_ERR_INVALID, "gsp_scale_drain_events: the engine records no events "
+                "(gsp_scale_params.events = 0)");
+    if (int rc = gsp_scale_sync(s)) return rc;
+    int64_t total = 0, dropped = 0;
+    for (Shard &sh : s->local) {
+        unsigned long long c = 0;
+        GSP_HIP(hipMemcpy(&c, sh.ev_count.p, 8, hipMemcpyDeviceToHost));
+        const int64_t have = std::min<int64_t>(int64_t(c), s->ev_cap);
+        dropped += int64_t(c) - have;
+        if (buf && total < cap && have > 0)
+            GSP_HIP(hipMemcpy(buf + total, sh.ev_buf.p, size_t(std::min(have, cap - total)) * 8,
+                              hipMemcpyDeviceToHost));
+        total += have;
+        if (buf) GSP_HIP(hipMemset(sh.ev_count.p, 0, 8));
+    }
+    *n = total;
+    if (lost) *lost = dropped;
     return GSP_OK;
 }
 

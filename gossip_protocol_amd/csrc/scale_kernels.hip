@@ -18,6 +18,7 @@
 #include "wave_ops.hpp"
 
 namespace gsp {
+
 namespace {
 
 __device__ inline uint64_t event_mix(uint32_t kind, uint32_t t, uint32_t r, uint32_t x) {
@@ -488,6 +489,7 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             slow = ev != 0;
             bits = q;
         }
+        uint32_t evj = 0, evr = 0;            // this chunk's join / remove entries (event stream)
         if (kInit || slow) {
             bits = 0;
 #pragma unroll
@@ -501,14 +503,27 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                         hsum += event_mix(2, uint32_t(t), uint32_t(r), uint32_t(gc0 + i));
                         ws[i >> 1] &= ~(0xFFFFu << sh);
                         ent = 0;
+                        evr |= 1u << i;
                     } else if (!before) {
                         joins++;
                         hsum += event_mix(1, uint32_t(t), uint32_t(r), uint32_t(gc0 + i));
+                        evj |= 1u << i;
                     }
                 }
                 const bool counted = ent && (!kTfail || ((t5 - ent) & 31u) < tf);
                 bits |= (counted ? 1u : 0u) << i;
             }
+        }
+        if (!kInit && a.ev_buf) {             // the event stream: this chunk's records
+            const uint32_t both = evj | (evr << 8);
+            wave_append_events(a.ev_buf, a.ev_count, a.ev_cap, uint32_t(__builtin_popcount(both)),
+                               [&](uint32_t i) {
+                                   uint32_t m = both;
+                                   for (uint32_t z = 0; z < i; ++z) m &= m - 1;
+                                   const uint32_t b = uint32_t(__builtin_ffs(m) - 1);
+                                   return event_record(b < 8 ? 1u : 2u, uint32_t(t), uint32_t(r),
+                                                       uint32_t(gc0 + (b & 7u)));
+                               });
         }
         live += __builtin_popcount(bits);
         st16<kNtOwn>(own_cur + lc0, ws);

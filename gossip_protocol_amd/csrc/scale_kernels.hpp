@@ -68,10 +68,47 @@ struct ScaleTickArgs {
     int32_t *ping;               // swim: [rows] probe target of the last send (-1 none)
     uint8_t *bitmap;             // slice mode: [rows][stride / 8] presence bits
     unsigned long long *dig;     // [kDigSlots][kDigFields] of this tick
+    // event stream (gsp_scale_params.events): every join / remove as one 64-bit record
+    // kind << 62 | t << 42 | r << 21 | x (event_record), appended in wave-compacted runs
+    unsigned long long *ev_buf;  // [ev_cap] (null: events off)
+    unsigned long long *ev_count;// [1] records appended since the last drain (may exceed ev_cap:
+                                 // the excess is lost and reported by the drain)
+    int64_t ev_cap;
     int32_t *err;                // [1] capacity error: 0, else the first tick a receiver got
                                  // more than max_segment messages (every later tick is a no-op)
     int32_t max_segment;         // <= kMaxSegment (lowered only by tests, GSP_TEST_MAX_SEGMENT)
 };
+
+__host__ __device__ inline unsigned long long event_record(uint32_t kind, uint32_t t, uint32_t r,
+                                                           uint32_t x) {
+    return (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFFu) << 42) | (uint64_t(r & 0x1FFFFFu) << 21) |
+           uint64_t(x & 0x1FFFFFu);
+}
+
+// Reserve `cnt` ring slots for this lane: one wave prefix and one atomic per wave; returns
+// the lane's first slot (slots >= cap are lost).  Call from converged code.
+__device__ inline uint64_t wave_reserve_events(unsigned long long *count, uint32_t cnt) {
+    if (!__ballot(cnt > 0)) return 0;                  // wave-uniform
+    uint32_t incl = cnt;                               // inclusive wave scan (DPP-free form)
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(incl, d, 64);
+        if ((threadIdx.x & 63) >= uint32_t(d)) incl += u;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    unsigned long long base = 0;
+    if ((threadIdx.x & 63) == 63) base = atomicAdd(count, (unsigned long long)total);
+    base = __shfl(base, 63, 64);
+    return base + (incl - cnt);
+}
+
+// Append this lane's `cnt` records (rec(i), i < cnt) to the ring (wave_reserve_events).
+template <typename Rec>
+__device__ inline void wave_append_events(unsigned long long *buf, unsigned long long *count,
+                                          int64_t cap, uint32_t cnt, Rec &&rec) {
+    uint64_t p = wave_reserve_events(count, cnt);
+    for (uint32_t i = 0; i < cnt; ++i, ++p)
+        if (int64_t(p) < cap) buf[p] = rec(i);
+}
 
 // merge: 0 = per-entry scalar form, 1 = packed 16-bit form (v_pk_* / v_bfi_b32)
 hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st);

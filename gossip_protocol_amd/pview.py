@@ -107,6 +107,10 @@ class PviewEngine:
                                        n.value, ctypes.byref(n)), "gsp_pview_messages")
         return buf[:n.value].reshape(-1, self.fanout)
 
+    def drain_events(self):
+        """(records, lost) since the last drain (events=True); see _lib.split_events."""
+        return _lib.drain_events(lib().gsp_pview_drain_events, self._h)
+
     def perf(self):
         p = _lib.GspScalePerf()
         check(lib().gsp_pview_perf_get(self._h, ctypes.byref(p)), "gsp_pview_perf_get")

@@ -145,6 +145,10 @@ class ScaleEngine:
     def set_cache_policy(self, policy):
         check(lib().gsp_scale_set_cache_policy(self._h, int(policy)), "gsp_scale_set_cache_policy")
 
+    def drain_events(self):
+        """(records, lost) since the last drain (events=True); see _lib.split_events."""
+        return _lib.drain_events(lib().gsp_scale_drain_events, self._h)
+
     def stream(self):
         s = ctypes.c_void_p()
         check(lib().gsp_scale_hip_stream(self._h, ctypes.byref(s)), "gsp_scale_hip_stream")

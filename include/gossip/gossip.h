@@ -352,6 +352,23 @@ int gsp_scale_set_merge(gsp_scale *s, int32_t packed);
 int gsp_scale_hip_stream(gsp_scale *s, void **stream);
 
 /* ------------------------------------------------------------------------------------
+ * Event stream (params.events = 1): the tick kernels append every join / remove (partial
+ * view: and evict) as one 64-bit record kind << 62 | t << 42 | r << 21 | x (kind 1 join,
+ * 2 remove, 3 evict; r = the node whose list changed, x = the member), wave-compacted into a
+ * device ring -- the scale form of Log::logNodeAdd / logNodeRemove (Log.cpp:116-130).
+ * drain: copies the records of every tick since the last drain (device order) into buf (at
+ * most cap), sets *n to their number and *lost to the records the ring could not hold, and
+ * empties the ring; buf = NULL only counts (the ring is kept).
+ * ---------------------------------------------------------------------------------- */
+int gsp_scale_drain_events(gsp_scale *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
+/* Appends event records as the reference's dbg.log lines (Log.cpp:44-130): "\n <r> [t] Node
+ * <x> joined at time t" ("removed", "evicted"), addresses printed as Log.cpp:73 does (id =
+ * index + 1 in signed bytes, port 0), in a canonical order -- t ascending, r descending (the
+ * phase-P order of Application.cpp:138), joins then removes then evictions, x ascending.  A
+ * new file starts with the "131" header (Log.cpp:79-88).  ev is sorted in place. */
+int gsp_events_write_log(uint64_t *ev, int64_t n, const char *path);
+
+/* ------------------------------------------------------------------------------------
  * PARTIAL-VIEW engine (BASELINE config 5): every node keeps at most `view` member entries
  * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (ascending
  * sender; the rest are counted as overflow); after the TREMOVE scan a view larger than
@@ -402,6 +419,8 @@ int gsp_pview_row(gsp_pview *s, int32_t r, uint64_t *buf, int32_t cap, int32_t *
 int gsp_pview_own_hb(gsp_pview *s, int32_t r, int32_t *hb);
 int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);
+/* As gsp_scale_drain_events (join / remove / evict records). */
+int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
 
 #ifdef __cplusplus
 }

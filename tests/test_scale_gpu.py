@@ -183,15 +183,18 @@ def test_swim_matches_oracle(case, shards, layout, merge, tfail, swim):
     plain.close()
 
 
-def test_rccl_rank_path_one_rank():
+@pytest.mark.parametrize("swim", [0, 2])
+@pytest.mark.parametrize("tfail", [0, 5])
+def test_rccl_rank_path_one_rank(tfail, swim):
     """The RCCL code path (ncclCommInitRank, all-gather, all-reduce MAX) with a world of one:
-    a one-rank communicator still runs the column protocol and must match the oracle."""
+    a one-rank communicator still runs the column protocol and must match the oracle, with
+    TFAIL suspicion and SWIM probing (whose probe results cross the same all-reduce) on."""
     from gossip_protocol_amd.scale import nccl_unique_id
     n, ticks = 1024, 16
-    orc = ScaleOracle(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5,
-                      fail_ppm=20000, seed=4)
-    with ScaleEngine(n, fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5, fail_ppm=20000,
-                     seed=4, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id()) as eng:
+    kw = dict(fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5, fail_ppm=20000, seed=4,
+              tfail=tfail, swim=swim)
+    orc = ScaleOracle(n, **kw)
+    with ScaleEngine(n, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id(), **kw) as eng:
         for t in range(1, ticks + 1):
             want = orc.step()
             eng.step(1)
