@@ -255,8 +255,9 @@ def _pview_valu(nodes, world, kern_ms):
     """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per launch from the
     committed PMC pass (profiles/pmc_sq_pview.json, scripts/gpu_run.sh) over the live mean
     kernel time: wave64 VALU instructions issued per SIMD cycle (1,024 SIMDs at 2.4 GHz), and
-    that rate against the 4-cycle wave64 issue model (MI355X_MICROARCH.md, 'vector-instruction
-    ISSUE cost'); one GPU, config 5 only."""
+    that rate against the SIMD's issue ceiling -- one wave64 VALU instruction per 2 cycles
+    with two or more waves resident (MI355X_MICROARCH.md, "Wave scheduling" and the
+    v_fma_f32 row of the constants table; 4 cycles is one wave alone); config 5, one GPU."""
     prof = os.path.join(ROOT, "profiles", "pmc_sq_pview.json")
     if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
         return None
@@ -266,16 +267,23 @@ def _pview_valu(nodes, world, kern_ms):
         return None
     per_cycle = insts / (1024 * 2.4e9 * kern_ms * 1e-3)
     return {"bound": "valu-issue", "insts_per_launch": insts, "insts_per_simd_cycle": per_cycle,
-            "frac_of_4cycle_issue": per_cycle * 4.0, "clock_ghz": 2.4}
+            "frac_of_2cycle_issue": per_cycle * 2.0, "clock_ghz": 2.4}
 
 
-def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
+EVENT_CAP = 1 << 26          # records per shard (512 MB): config 3's ~42.5 M removes fit
+
+
+def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=False):
     """Full-view workload (config 3 rules) on `world` GPUs: one GPU fused, or column / row
-    shards.  Returns job totals (time and kernel time are the slowest rank's)."""
+    shards.  Returns job totals (time and kernel time are the slowest rank's).  events: the
+    tick kernels also append every join / remove record to the device ring (drained after
+    the timed region; event_summary)."""
     import torch
     from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
     kw = dict(fanout=FANOUT, fail_mode=FAIL_RANDOM, fail_tick=FAIL_TICK, fail_ppm=FAIL_PPM,
               seed=SEED, max_ticks=warmup + steps, layout=layout)
+    if events:
+        kw.update(events=True, event_cap=EVENT_CAP)
     if dist is not None:
         from gossip_protocol_amd.dist import make_rank_engine
         eng = make_rank_engine(nodes, local, **kw)
@@ -283,6 +291,8 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
         eng = ScaleEngine(nodes, device=local, **kw)
     eng.step(warmup)
     eng.sync()
+    if events:
+        eng.drain_events()                # the warm-up ticks' records (none: crash at t = 10)
     perf0 = eng.perf()
     if dist is not None:
         dist.barrier()
@@ -306,6 +316,7 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
     launches = max(perf1["merge_launches"] - perf0["merge_launches"], 1)
     kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / launches
     csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / launches
+    ev = event_summary(eng, nodes, warmup + steps, dist) if events else None
     eng.close()
     if dist is not None:
         # per-row counts live on rank 0 only (columns) or on the row's owner (rows): the sum is
@@ -325,7 +336,53 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns"):
     slices = world if layout == "columns" else 1
     bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
     return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
-            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout}
+            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout,
+            "events": ev}
+
+
+def event_summary(eng, nodes, last_tick, dist):
+    """Per-crashed-node detection latency from the drained event stream: for every node x that
+    some node removed, the tick of the first removal of x and of the last one (every live
+    node has removed it), minus the crash tick.  The reference logs the same removals as
+    "Node x removed at time t" lines (MP1Node.cpp:343, Log.cpp:127-130); the grader measures
+    detection from them (grader/Grader.sh).  Ranks combine per-node first / last / count."""
+    import numpy as np
+    import torch
+    from gossip_protocol_amd import _lib
+    rec, lost = eng.drain_events()
+    kind, tk, _, x = _lib.split_events(rec)
+    rem = kind == _lib.EVENT_REMOVE
+    xr, tr = x[rem], tk[rem]
+    first = np.full(nodes, 1 << 30, np.int64)
+    last = np.full(nodes, -1, np.int64)
+    for t in np.unique(tr)[::-1]:         # descending: the earliest tick is written last
+        first[xr[tr == t]] = t
+    for t in np.unique(tr):
+        last[xr[tr == t]] = t
+    count = np.bincount(xr, minlength=nodes).astype(np.int64)
+    joins = int((kind == _lib.EVENT_JOIN).sum())
+    if dist is not None:
+        f = torch.from_numpy(first).to(_dev())
+        l_ = torch.from_numpy(last).to(_dev())
+        c = torch.from_numpy(count).to(_dev())
+        tot = torch.tensor([len(rec), lost, joins], dtype=torch.int64, device=_dev())
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        dist.all_reduce(l_, op=dist.ReduceOp.MAX)
+        dist.all_reduce(c)
+        dist.all_reduce(tot)
+        first, last, count = f.cpu().numpy(), l_.cpu().numpy(), c.cpu().numpy()
+        n_rec, lost, joins = (int(v) for v in tot.tolist())
+    else:
+        n_rec = len(rec)
+    det = count > 0
+    stat = lambda a: {"min": int(a.min()), "mean": float(a.mean()), "max": int(a.max())} \
+        if len(a) else None
+    return {"records": n_rec, "lost": int(lost), "joins": joins, "removes": int(count.sum()),
+            "crash_tick": FAIL_TICK, "last_tick": last_tick,
+            "crashed_nodes_detected": int(det.sum()),
+            "removes_per_detected_node": float(count[det].mean()) if det.any() else 0.0,
+            "first_detection_latency_ticks": stat(first[det] - FAIL_TICK),
+            "full_detection_latency_ticks": stat(last[det] - FAIL_TICK)}
 
 
 def summarize_full(r, nodes, steps, world):
@@ -382,6 +439,8 @@ def main(argv=None):
     ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item (N > 1)")
     ap.add_argument("--item-budget", type=int, default=420,
                     help="seconds for the secondary line items before the line is printed as is")
+    ap.add_argument("--no-events", action="store_true",
+                    help="skip the event-stream run (detection latency, recording cost)")
     ap.add_argument("--no-rows", action="store_true",
                     help="skip the full-view row-layout line items (N > 1)")
     args = ap.parse_args(argv)
@@ -436,6 +495,19 @@ def main(argv=None):
             else:
                 out.setdefault(key, {})[sub] = res
 
+    # the same headline workload with the event stream on: kernel-time cost of recording
+    # every join / remove on the device, and the detection latency read from the records
+    def _events_item():
+        r = run_full(args.nodes, args.steps, args.warmup, world, local, dist, events=True)
+        if r is None or out is None:
+            return None
+        ev = r["events"]
+        ev.update({"kernel_ms": r["kern_ms"], "kernel_ms_events_off": full["kern_ms"],
+                   "kernel_overhead_frac": r["kern_ms"] / full["kern_ms"] - 1.0,
+                   "value_events_on": r["rounds"] / r["el"]})
+        return ev
+    if not args.no_events:
+        item("events", _events_item)
     if not args.no_pview:
         item("pview", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world,
                                         local, dist, not args.no_cpu_baseline))

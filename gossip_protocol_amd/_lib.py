@@ -197,6 +197,8 @@ class GspError(RuntimeError):
 
 
 EVENT_JOIN, EVENT_REMOVE, EVENT_EVICT = 1, 2, 3
+# params.events: 0 off, EVENTS_ALL, or an OR of the kind bits (bit k = record kind k)
+EVENTS_ALL, EVENTS_JOIN, EVENTS_REMOVE, EVENTS_EVICT = 1, 2, 4, 8
 
 
 def drain_events(fn, handle):

@@ -40,7 +40,8 @@ struct PvShard {
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok;
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
-    gsp::DevBuf<unsigned long long> dig, prof, rowdig, ev_buf, ev_count;
+    gsp::DevBuf<unsigned long long> dig, prof, rowdig;
+    gsp::EvRing ev;
     gsp::RowxBufs x;             // row exchange (G > 1)
 
     void release() {
@@ -54,8 +55,7 @@ struct PvShard {
         dig.release();
         prof.release();
         rowdig.release();
-        ev_buf.release();
-        ev_count.release();
+        ev.release();
     }
 };
 
@@ -75,7 +75,6 @@ struct gsp_pview {
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
-    int64_t ev_cap = 0;          // event ring capacity per shard (events on)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail, h_start;
@@ -138,9 +137,7 @@ struct gsp_pview {
         a.order = sort_rows ? sh.order.p : nullptr;
         a.prof = sh.prof.p;
         a.waves = waves;
-        a.ev_buf = p.events ? sh.ev_buf.p : nullptr;
-        a.ev_count = sh.ev_count.p;
-        a.ev_cap = ev_cap;
+        a.ev = sh.ev.args();
         return a;
     }
 
@@ -191,7 +188,7 @@ int pview_validate(const gsp_pview_params *p) {
     GSP_REQUIRE(p->tfail == 0 || (p->tfail >= 1 && p->tfail < p->tremove), GSP_ERR_INVALID,
                 "tfail=%d: 0 (off) or 1..tremove-1", p->tfail);
     GSP_REQUIRE(p->swim >= 0 && p->swim <= 8, GSP_ERR_INVALID, "swim=%d: 0 (off) or 1..8 paths", p->swim);
-    GSP_REQUIRE(p->events == 0 || p->events == 1, GSP_ERR_INVALID, "events=%d", p->events);
+    GSP_REQUIRE(p->events >= 0 && p->events <= 15, GSP_ERR_INVALID, "events=%d: 0 off, 1 all, or an OR of GSP_EVENTS_*", p->events);
     GSP_REQUIRE(p->event_cap >= 0, GSP_ERR_INVALID, "event_cap=%lld", (long long)p->event_cap);
     return gsp::validate_policy(p->policy, p->n);
 }
@@ -242,11 +239,7 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
         GSP_HIP(hipMemsetAsync(sh.table[1].p, 0xFF, rows * size_t(V) * 8, st));
         if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(V)));
     }
-    if (s->p.events) {
-        GSP_HIP(sh.ev_buf.alloc(size_t(s->ev_cap)));
-        GSP_HIP(sh.ev_count.alloc(1));
-        GSP_HIP(hipMemsetAsync(sh.ev_count.p, 0, 8, st));
-    }
+    if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
@@ -373,7 +366,6 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
-    s->ev_cap = p->events ? (p->event_cap > 0 ? p->event_cap : (int64_t(1) << 24)) : 0;
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
@@ -597,17 +589,7 @@ int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n,
                 "(gsp_pview_params.events = 0)");
     if (int rc = gsp_pview_sync(s)) return rc;
     int64_t total = 0, dropped = 0;
-    for (PvShard &sh : s->local) {
-        unsigned long long c = 0;
-        GSP_HIP(hipMemcpy(&c, sh.ev_count.p, 8, hipMemcpyDeviceToHost));
-        const int64_t have = std::min<int64_t>(int64_t(c), s->ev_cap);
-        dropped += int64_t(c) - have;
-        if (buf && total < cap && have > 0)
-            GSP_HIP(hipMemcpy(buf + total, sh.ev_buf.p, size_t(std::min(have, cap - total)) * 8,
-                              hipMemcpyDeviceToHost));
-        total += have;
-        if (buf) GSP_HIP(hipMemset(sh.ev_count.p, 0, 8));
-    }
+    for (PvShard &sh : s->local) GSP_HIP(sh.ev.drain(buf, cap, &total, &dropped));
     *n = total;
     if (lost) *lost = dropped;
     return GSP_OK;

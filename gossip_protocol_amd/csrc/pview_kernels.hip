@@ -421,10 +421,15 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
     }
 
-    if (a.ev_buf) {                                      // event stream: joins and removes
-        uint64_t p = wave_reserve_events(a.ev_count, uint32_t(__popc(jmask) + __popc(rmask) + __popc(adopt)));
+    if (a.ev.buf) {                                      // event stream: joins and removes
+        if (!(a.ev.kinds & GSP_EVENTS_JOIN)) jmask = 0;
+        if (!(a.ev.kinds & GSP_EVENTS_REMOVE)) rmask = 0;
+        const uint32_t amask = (a.ev.kinds & GSP_EVENTS_JOIN) ? adopt : 0u;
+        uint64_t p = wave_reserve_events(ev_stripe_count(a.ev),
+                                         uint32_t(__popc(jmask) + __popc(rmask) + __popc(amask)));
+        unsigned long long *const eb = ev_stripe_buf(a.ev);
         auto put = [&](uint32_t kind, uint32_t x) {
-            if (int64_t(p) < a.ev_cap) a.ev_buf[p] = event_record(kind, t, uint32_t(r), x);
+            if (int64_t(p) < a.ev.cap) eb[p] = event_record(kind, t, uint32_t(r), x);
             ++p;
         };
 #pragma unroll
@@ -434,7 +439,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
 #pragma unroll
         for (int jj = 0; jj < kJ; ++jj)
-            if ((adopt >> jj) & 1u) put(1u, ssrc[jj]);
+            if ((amask >> jj) & 1u) put(1u, ssrc[jj]);
     }
     pm.mark(3);
     // ---- 5a. survivors (and adopted orphans), compacted in id order -------------------------
@@ -585,10 +590,11 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
-        if (a.ev_buf) {
+        const bool ev_on = a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
+        if (ev_on) {
             const int32_t tk = int32_t(need2) - int32_t(tie_before);
             const uint32_t kept = nk + uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
-            evp = wave_reserve_events(a.ev_count, nloc - kept);
+            evp = wave_reserve_events(ev_stripe_count(a.ev), nloc - kept);
         }
         for_each([&](uint32_t v, uint32_t x, uint32_t b) {
             const uint32_t hb = v >> 5;
@@ -601,8 +607,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             } else {
                 evicts++;
                 hsum += pv_hash(S_evict, x);
-                if (a.ev_buf) {
-                    if (int64_t(evp) < a.ev_cap) a.ev_buf[evp] = event_record(3u, t, uint32_t(r), x);
+                if (ev_on) {
+                    if (int64_t(evp) < a.ev.cap) ev_stripe_buf(a.ev)[evp] = event_record(3u, t, uint32_t(r), x);
                     ++evp;
                 }
             }

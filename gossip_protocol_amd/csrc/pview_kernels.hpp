@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "event_ring.hpp"
+
 namespace gsp {
 
 constexpr int kPvBlock = 256;
@@ -49,9 +51,7 @@ struct PviewTickArgs {
     int32_t *err;                // [1] capacity error: 0, else the first tick a receiver was
                                  // sent more than max_segment messages (the job stops there)
     int32_t max_segment;         // <= kPvMaxSegment (lowered only by tests)
-    unsigned long long *ev_buf;  // event stream (null: off): join / remove / evict records
-    unsigned long long *ev_count;// [1] records appended since the last drain
-    int64_t ev_cap;
+    EvRingArgs ev;               // event stream (ev.buf null: off), event_ring.hpp
     const int32_t *kcount;       // [8] rows per merged-message count k (or null: row order)
     const int32_t *order;        // [8][rows]: the rows of each k; workgroup b runs the b-th row
                                  // of the k-descending order (one code variant per CU stretch)

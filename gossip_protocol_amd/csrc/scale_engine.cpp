@@ -39,7 +39,8 @@ struct Shard {
         ping, deg, off, fill, csr_src, err, tile_sum, start_tick, joiners, join_ok;
     gsp::DevBuf<uint16_t> intro_buf;   // row layout, shards != 0: node 0's row of the last tick
     gsp::DevBuf<uint8_t> bitmap;
-    gsp::DevBuf<unsigned long long> dig, ev_buf, ev_count;
+    gsp::DevBuf<unsigned long long> dig;
+    gsp::EvRing ev;
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
@@ -49,8 +50,7 @@ struct Shard {
         intro_buf.release();
         bitmap.release();
         dig.release();
-        ev_buf.release();
-        ev_count.release();
+        ev.release();
         x.release();
     }
 };
@@ -70,7 +70,6 @@ struct gsp_scale {
     int32_t *h_err = nullptr;  // pinned mirror of the shards' capacity flags, refreshed by an
                                // async copy at the end of every gsp_scale_step call
     int32_t max_segment = gsp::kMaxSegment;
-    int64_t ev_cap = 0;        // event ring capacity per shard (events on)
     ncclComm_t comm = nullptr; // one shard per process when set
     int64_t width = 0;         // n rounded up to 2048 * G
     int64_t stride = 0;        // columns per shard
@@ -78,6 +77,7 @@ struct gsp_scale {
     bool timing = true;
     int policy = 5;            // bit 0 nt own row, bit 1 nt sender rows, bit 2 pipelined loads
     int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
+    int32_t lds_pad = 0;       // GSP_SCALE_LDS_PAD: extra LDS per tick-kernel workgroup
     std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
     std::vector<int32_t> h_fail, h_start;
     bool joins = false;        // a join schedule is set (some node starts after tick 0)
@@ -115,6 +115,7 @@ struct gsp_scale {
         a.nt_own = policy & 1;
         a.nt_src = (policy >> 1) & 1;
         a.pipe = (policy >> 2) & 1;
+        a.lds_pad = lds_pad;
         a.tfail = p.tfail;
         a.swim = p.swim;
         a.count_rounds = rowmode || sh.g == 0;
@@ -143,9 +144,7 @@ struct gsp_scale {
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
         a.max_segment = max_segment;
-        a.ev_buf = p.events ? sh.ev_buf.p : nullptr;
-        a.ev_count = sh.ev_count.p;
-        a.ev_cap = ev_cap;
+        a.ev = sh.ev.args();
         return a;
     }
 
@@ -199,7 +198,7 @@ int validate_scale_params(const gsp_scale_params *p) {
     GSP_REQUIRE(p->max_ticks >= 1 && int64_t(p->h0) + p->max_ticks <= 2047, GSP_ERR_RANGE,
                 "h0 + max_ticks = %d exceeds the 11-bit packed heartbeat (2047)",
                 p->h0 + p->max_ticks);
-    GSP_REQUIRE(p->events == 0 || p->events == 1, GSP_ERR_INVALID, "events=%d", p->events);
+    GSP_REQUIRE(p->events >= 0 && p->events <= 15, GSP_ERR_INVALID, "events=%d: 0 off, 1 all, or an OR of GSP_EVENTS_*", p->events);
     GSP_REQUIRE(p->event_cap >= 0, GSP_ERR_INVALID, "event_cap=%lld", (long long)p->event_cap);
     return validate_policy(p->policy, p->n);
 }
@@ -243,11 +242,7 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(sh.dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
-    if (s->p.events) {
-        GSP_HIP(sh.ev_buf.alloc(size_t(s->ev_cap)));
-        GSP_HIP(sh.ev_count.alloc(1));
-        GSP_HIP(hipMemsetAsync(sh.ev_count.p, 0, 8, st));
-    }
+    if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
     if (s->joins) {
         GSP_HIP(sh.start_tick.alloc(size_t(n)));
         GSP_HIP(hipMemcpyAsync(sh.start_tick.p, s->h_start.data(), size_t(n) * 4, hipMemcpyHostToDevice, st));
@@ -482,17 +477,18 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                                        int64_t(double(rows_max) * p->fanout / shards * 1.25) + 4096);
     }
     s->h_fail = gsp::scale_fail_ticks(*p);
-    s->ev_cap = p->events ? (p->event_cap > 0 ? p->event_cap : (int64_t(1) << 24)) : 0;
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
     if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 7;
+    if (const char *pad = std::getenv("GSP_SCALE_LDS_PAD")) s->lds_pad = std::max(0, std::min(65536, std::atoi(pad)));
     if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
     if (!s->sliced) {
-        // the fused kernel keeps the row's presence bitmap in LDS next to 8.3 KB of statics
-        GSP_REQUIRE(gsp::scale_lds_bytes(s->stride, false) <= 48 * 1024, GSP_ERR_CAPACITY,
-                    "row bitmap of %lld B exceeds the LDS budget (one-GPU full view n <= 393216)",
-                    (long long)(s->stride / 8));
+        // the fused kernel keeps the row's presence bitmap (and the event stage) in LDS next
+        // to 8.3 KB of statics
+        GSP_REQUIRE(gsp::scale_lds_bytes(s->stride, false, p->events != 0) <= 48 * 1024, GSP_ERR_CAPACITY,
+                    "row bitmap of %lld B%s exceeds the LDS budget (one-GPU full view n <= 393216, "
+                    "327680 with events)", (long long)(s->stride / 8), p->events ? " + event stage" : "");
     }
     if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
         s->max_segment = std::max(1, std::min(gsp::kMaxSegment, std::atoi(ms)));
@@ -786,17 +782,7 @@ int gsp_scale_drain_events(gsp_scale *s, uint64_t *buf, int64_t cap, int64_t *n,
                 "(gsp_scale_params.events = 0)");
     if (int rc = gsp_scale_sync(s)) return rc;
     int64_t total = 0, dropped = 0;
-    for (Shard &sh : s->local) {
-        unsigned long long c = 0;
-        GSP_HIP(hipMemcpy(&c, sh.ev_count.p, 8, hipMemcpyDeviceToHost));
-        const int64_t have = std::min<int64_t>(int64_t(c), s->ev_cap);
-        dropped += int64_t(c) - have;
-        if (buf && total < cap && have > 0)
-            GSP_HIP(hipMemcpy(buf + total, sh.ev_buf.p, size_t(std::min(have, cap - total)) * 8,
-                              hipMemcpyDeviceToHost));
-        total += have;
-        if (buf) GSP_HIP(hipMemset(sh.ev_count.p, 0, 8));
-    }
+    for (Shard &sh : s->local) GSP_HIP(sh.ev.drain(buf, cap, &total, &dropped));
     *n = total;
     if (lost) *lost = dropped;
     return GSP_OK;

@@ -259,6 +259,8 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     __shared__ int32_t s_jc[kMaxIntro];      // JOINREP payload: chosen columns / entries
     __shared__ uint32_t s_jv[kMaxIntro];
     __shared__ int32_t s_njc;
+    __shared__ uint32_t s_evf[4];            // event stream: staged records per wave
+    __shared__ unsigned long long s_evbase;
 
     const int32_t tid = threadIdx.x;
     const int32_t lane = tid & 63, wave = tid >> 6;
@@ -353,6 +355,24 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     uint16_t *own_cur = a.cur + int64_t(lr) * stride;
     uint32_t live = 0, joins = 0, removes = 0;
     uint64_t hsum = 0;
+    // event stream: each wave stages its records as kind << 30 | column in LDS (after the
+    // bitmap, kEvStage words per wave) and the row takes one ring reservation at its end; a
+    // wave whose stage would overflow flushes it with a reservation of its own
+    uint32_t *const s_ev = s_bits + (kSlice ? 4 : (stride >> 5)) + wave * kEvStage;
+    uint32_t ev_fill = 0;                                           // wave-uniform
+    unsigned long long *const ev_buf = a.ev.buf ? ev_stripe_buf(a.ev) : nullptr;
+    unsigned long long *const ev_count = ev_stripe_count(a.ev);
+    auto ev_flush = [&](uint32_t fill, unsigned long long base) {   // fill records -> ring
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = uint32_t(lane); i < fill; i += 64) {
+            const uint32_t s = s_ev[i];
+            if (int64_t(base + i) < a.ev.cap)
+                ev_buf[base + i] = event_record(s >> 30, uint32_t(t), uint32_t(r), s & 0x3FFFFFFFu);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
 
     // kPipe: the first 4 sender rows as wave-uniform (scalar) pointers, and the request of one
     // chunk's own + sender vectors (16 B per lane each) issued one chunk ahead
@@ -514,16 +534,28 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                 bits |= (counted ? 1u : 0u) << i;
             }
         }
-        if (!kInit && a.ev_buf) {             // the event stream: this chunk's records
-            const uint32_t both = evj | (evr << 8);
-            wave_append_events(a.ev_buf, a.ev_count, a.ev_cap, uint32_t(__builtin_popcount(both)),
-                               [&](uint32_t i) {
-                                   uint32_t m = both;
-                                   for (uint32_t z = 0; z < i; ++z) m &= m - 1;
-                                   const uint32_t b = uint32_t(__builtin_ffs(m) - 1);
-                                   return event_record(b < 8 ? 1u : 2u, uint32_t(t), uint32_t(r),
-                                                       uint32_t(gc0 + (b & 7u)));
-                               });
+        if (!kInit && ev_buf) {               // the event stream: stage this chunk's records
+            uint32_t both = ((a.ev.kinds & GSP_EVENTS_JOIN) ? evj : 0u) |
+                            ((a.ev.kinds & GSP_EVENTS_REMOVE) ? (evr << 8) : 0u);
+            const uint32_t cnt = uint32_t(__builtin_popcount(both));
+            if (__ballot(cnt > 0)) {          // wave-uniform
+                const uint32_t incl = wave_incl_scan(cnt);
+                const uint32_t total = lane_of(incl, 63);
+                if (ev_fill + total > uint32_t(kEvStage)) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(ev_count, (unsigned long long)ev_fill);
+                    base = (uint64_t(lane_of(uint32_t(base >> 32), 0)) << 32) | lane_of(uint32_t(base), 0);
+                    ev_flush(ev_fill, base);
+                    ev_fill = 0;
+                }
+                uint32_t p = ev_fill + incl - cnt;
+                while (both) {
+                    const uint32_t b = uint32_t(__builtin_ffs(both) - 1);
+                    both &= both - 1;
+                    s_ev[p++] = ((b < 8 ? 1u : 2u) << 30) | uint32_t(gc0 + (b & 7u));
+                }
+                ev_fill += total;
+            }
         }
         live += __builtin_popcount(bits);
         st16<kNtOwn>(own_cur + lc0, ws);
@@ -538,8 +570,18 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     const uint64_t v0 = wave_sum_u64(live), v1 = wave_sum_u64(joins), v2 = wave_sum_u64(removes);
     const uint64_t v3 = wave_sum_u64(hsum);
     if (lane == 0) { s_red[wave][0] = v0; s_red[wave][1] = v1; s_red[wave][2] = v2; s_red[wave][3] = v3; }
+    if (!kInit && ev_buf && lane == 0) s_evf[wave] = ev_fill;
     __syncthreads();
     const uint64_t tot_live = s_red[0][0] + s_red[1][0] + s_red[2][0] + s_red[3][0];
+    if (!kInit && ev_buf) {                   // the row's one ring reservation
+        const uint32_t f0 = s_evf[0], f1 = s_evf[1], f2 = s_evf[2], f3 = s_evf[3];
+        if (tid == 0 && f0 + f1 + f2 + f3) s_evbase = atomicAdd(ev_count, (unsigned long long)(f0 + f1 + f2 + f3));
+        __syncthreads();
+        if (f0 + f1 + f2 + f3) {
+            const uint32_t before = (wave > 0 ? f0 : 0u) + (wave > 1 ? f1 : 0u) + (wave > 2 ? f2 : 0u);
+            ev_flush(ev_fill, s_evbase + before);
+        }
+    }
 
     unsigned long long *dig = a.dig + (blockIdx.x % kDigSlots) * kDigFields;
     if (tid == 0) {
@@ -802,11 +844,13 @@ unsigned grid_for(int64_t items, int64_t per_block, int64_t cap) {
 
 }  // namespace
 
-size_t scale_lds_bytes(int64_t stride, bool slice) { return slice ? 16 : size_t(stride / 8); }
+size_t scale_lds_bytes(int64_t stride, bool slice, bool events) {
+    return (slice ? 16 : size_t(stride / 8)) + (events ? size_t(4 * kEvStage * 4) : 0);
+}
 
 hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st) {
     if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    const size_t lds = scale_lds_bytes(a.stride, slice);
+    const size_t lds = scale_lds_bytes(a.stride, slice, false);
     if (slice)
         hipLaunchKernelGGL((scale_tick_kernel<true, true, 1, 0>), dim3(a.rows), dim3(kScaleBlock), lds, st, a);
     else if (a.swim > 0)
@@ -845,7 +889,7 @@ void launch_tick_policy(const ScaleTickArgs &a, int policy, size_t lds, hipStrea
 
 hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipStream_t st) {
     if (a.stride % kChunk || a.fanout < 1 || a.fanout > 16) return hipErrorInvalidValue;
-    const size_t lds = scale_lds_bytes(a.stride, slice);
+    const size_t lds = scale_lds_bytes(a.stride, slice, a.ev.buf != nullptr) + size_t(a.lds_pad);
     const int policy = (a.nt_own ? 1 : 0) | (a.nt_src ? 2 : 0);
     if (slice) {
         if (merge == 1) launch_tick_policy<true, 1>(a, policy, lds, st);

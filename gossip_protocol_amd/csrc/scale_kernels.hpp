@@ -16,11 +16,14 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "event_ring.hpp"
+
 namespace gsp {
 
 constexpr int kScaleBlock = 256;          // 4 waves
 constexpr int kEntriesPerLane = 8;        // 16 B per lane per row chunk
 constexpr int kChunk = kScaleBlock * kEntriesPerLane;   // 2048 columns per block iteration
+constexpr int kEvStage = 512;             // event stream: LDS-staged records per wave (one chunk's worst case)
 constexpr int kMaxSegment = 1024;         // messages one receiver can merge per tick
 constexpr int kDigSlots = 64;             // atomic sharding of the per-tick digest
 enum : int { kDigRounds = 0, kDigMerges, kDigSent, kDigDropped, kDigDelivered, kDigJoins,
@@ -42,6 +45,7 @@ struct ScaleTickArgs {
     int32_t h0;
     int32_t nt_own, nt_src;      // non-temporal policy of the own-row / sender-row streams
     int32_t pipe;                // software-pipelined chunk loads (packed merge, policy 1)
+    int32_t lds_pad;             // extra dynamic LDS bytes per workgroup (occupancy experiments)
     int32_t tfail;               // TFAIL suspicion: 0 off, else members this stale are not
                                  // gossiped / chosen / counted
     int32_t swim;                // SWIM probing: 0 off, else 1 direct + swim - 1 indirect paths
@@ -70,10 +74,7 @@ struct ScaleTickArgs {
     unsigned long long *dig;     // [kDigSlots][kDigFields] of this tick
     // event stream (gsp_scale_params.events): every join / remove as one 64-bit record
     // kind << 62 | t << 42 | r << 21 | x (event_record), appended in wave-compacted runs
-    unsigned long long *ev_buf;  // [ev_cap] (null: events off)
-    unsigned long long *ev_count;// [1] records appended since the last drain (may exceed ev_cap:
-                                 // the excess is lost and reported by the drain)
-    int64_t ev_cap;
+    EvRingArgs ev;               // event stream (ev.buf null: off), event_ring.hpp
     int32_t *err;                // [1] capacity error: 0, else the first tick a receiver got
                                  // more than max_segment messages (every later tick is a no-op)
     int32_t max_segment;         // <= kMaxSegment (lowered only by tests, GSP_TEST_MAX_SEGMENT)
@@ -146,6 +147,6 @@ hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, in
 // csr_src[off[d] + k] = sender, for every message slot i with out_dst[i] = d >= 0
 hipError_t launch_scatter(const int32_t *out_dst, int64_t slots, int32_t fanout, int32_t row0,
                           const int32_t *off, int32_t *fill, int32_t *csr_src, hipStream_t st);
-size_t scale_lds_bytes(int64_t stride, bool slice);
+size_t scale_lds_bytes(int64_t stride, bool slice, bool events);
 
 }  // namespace gsp

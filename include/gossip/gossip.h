@@ -253,10 +253,18 @@ typedef struct {
                            layout                                                      */
     gsp_policy policy;  /* join schedule + bounded introducer list, drop window, crash
                            events (all zero: off)                                      */
-    int32_t events;     /* 1: keep every join / remove event in a device ring, drained with
-                           gsp_scale_drain_events (Log.cpp:116-130's lines at scale)     */
-    int64_t event_cap;  /* ring capacity in events (0: 2^24)                            */
+    int32_t events;     /* event stream (Log.cpp:116-130's lines at scale), drained with
+                           gsp_scale_drain_events: 0 off, GSP_EVENTS_ALL, or an OR of
+                           GSP_EVENTS_JOIN / GSP_EVENTS_REMOVE                          */
+    int64_t event_cap;  /* ring capacity in events (0: 2^24; rounded up to a multiple of
+                           256, split evenly over 256 stripes)                          */
 } gsp_scale_params;
+
+/* params.events: which records the tick kernels keep (bit k = record kind k) */
+#define GSP_EVENTS_ALL 1      /* every kind the engine has                              */
+#define GSP_EVENTS_JOIN 2     /* kind 1: r added x (MP1Node.cpp:276, 297)               */
+#define GSP_EVENTS_REMOVE 4   /* kind 2: r removed x after TREMOVE (MP1Node.cpp:343)    */
+#define GSP_EVENTS_EVICT 8    /* kind 3: r's bounded view evicted x (partial view only) */
 
 typedef struct {
     int64_t tick, node_rounds, merges, sent, dropped, delivered, joins, removes;
@@ -352,13 +360,16 @@ int gsp_scale_set_merge(gsp_scale *s, int32_t packed);
 int gsp_scale_hip_stream(gsp_scale *s, void **stream);
 
 /* ------------------------------------------------------------------------------------
- * Event stream (params.events = 1): the tick kernels append every join / remove (partial
- * view: and evict) as one 64-bit record kind << 62 | t << 42 | r << 21 | x (kind 1 join,
- * 2 remove, 3 evict; r = the node whose list changed, x = the member), wave-compacted into a
- * device ring -- the scale form of Log::logNodeAdd / logNodeRemove (Log.cpp:116-130).
- * drain: copies the records of every tick since the last drain (device order) into buf (at
- * most cap), sets *n to their number and *lost to the records the ring could not hold, and
- * empties the ring; buf = NULL only counts (the ring is kept).
+ * Event stream (params.events != 0): the tick kernels append every join / remove (partial
+ * view: and evict) of the selected kinds as one 64-bit record kind << 62 | t << 42 | r << 21
+ * | x (kind 1 join, 2 remove, 3 evict; r = the node whose list changed, x = the member) --
+ * the scale form of Log::logNodeAdd / logNodeRemove (Log.cpp:116-130).  A row's records are
+ * staged in LDS and reserved in the ring at once; the ring is 256 stripes (row % 256), each
+ * with its own counter, so reservations do not queue on one address.
+ * drain: copies the records of every tick since the last drain (stripe by stripe, device
+ * order within a stripe) into buf (at most cap), sets *n to the number held and *lost to the
+ * records a full stripe could not hold, and empties the ring; buf = NULL only counts (the
+ * ring is kept).
  * ---------------------------------------------------------------------------------- */
 int gsp_scale_drain_events(gsp_scale *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
 /* Appends event records as the reference's dbg.log lines (Log.cpp:44-130): "\n <r> [t] Node
@@ -382,8 +393,8 @@ typedef struct {
     int32_t max_ticks;
     int32_t tfail, swim;  /* as gsp_scale_params: TFAIL suspicion, SWIM probing (0: off)   */
     gsp_policy policy;    /* as gsp_scale_params                                         */
-    int32_t events;       /* 1: keep every join / remove / evict event (gsp_pview_drain_events) */
-    int64_t event_cap;    /* ring capacity in events (0: 2^24)                            */
+    int32_t events;       /* as gsp_scale_params, with GSP_EVENTS_EVICT (gsp_pview_drain_events) */
+    int64_t event_cap;    /* as gsp_scale_params                                          */
 } gsp_pview_params;
 
 typedef struct {

@@ -45,6 +45,15 @@ class FakeEngine:
         return {"tick": t, "node_rounds": rows, "merges": 3 * rows, "delivered": 2 * rows,
                 "overflow": 0}
 
+    def drain_events(self):
+        """Removal records split over the ranks (kind 2 = remove, 1 = join): node 5 is removed
+        at ticks 12, 13 (rank 0) and 11 (rank 1), node 7 at 30 (rank 0) and 31 (rank 1)."""
+        import numpy as np
+        rec = {0: [(2, 12, 0, 5), (2, 13, 1, 5), (2, 30, 2, 7)],
+               1: [(2, 11, 600, 5), (2, 31, 601, 7), (1, 5, 600, 9)]}[self.rank]
+        return np.array([(k << 62) | (t << 42) | (r << 21) | x for k, t, r, x in rec],
+                        np.uint64), 0
+
     def layout(self):
         return (self.world, self.rank, self.n if self.rows else self.n // self.world)
 
@@ -112,3 +121,9 @@ def test_bench_two_ranks_gloo():
     assert abs(c3["value"] - 1024 * min(N_STEPS, 8) / (c3["ms_per_step"] * min(N_STEPS, 8) / 1e3)) \
         < 1e-6 * c3["value"]
     assert "skipped" in fr["config4"]                 # does not fit 2 GPUs
+    ev = d["events"]                                  # per-node first / last over the ranks
+    assert ev["records"] == 6 and ev["joins"] == 1 and ev["removes"] == 5 and ev["lost"] == 0
+    assert ev["crashed_nodes_detected"] == 2 and ev["removes_per_detected_node"] == 2.5
+    assert ev["first_detection_latency_ticks"] == {"min": 1, "mean": 10.5, "max": 20}
+    assert ev["full_detection_latency_ticks"] == {"min": 3, "mean": 12.0, "max": 21}
+    assert ev["kernel_overhead_frac"] == 0.0

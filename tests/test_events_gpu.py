@@ -27,12 +27,14 @@ def _multiset(kind, r, x):
     return sorted(zip(np.asarray(kind).tolist(), np.asarray(r).tolist(), np.asarray(x).tolist()))
 
 
-def _check_tick(eng, orc, t):
+def _check_tick(eng, orc, t, kinds=(1, 2, 3)):
     rec, lost = eng.drain_events()
     assert lost == 0
     k, tk, r, x = _lib.split_events(rec)
     assert np.all(tk == t), "tick field"
-    want = _multiset(*orc.events())
+    ok, orr, ox = orc.events()
+    keep = np.isin(ok, kinds)
+    want = _multiset(ok[keep], orr[keep], ox[keep])
     got = _multiset(k, r, x)
     assert got == want, "tick %d: %d events vs %d; first diff %s" % (
         t, len(got), len(want), next(((a, b) for a, b in zip(got, want) if a != b), None))
@@ -97,15 +99,41 @@ def test_partial_view_event_stream_matches_oracle(case):
     assert kinds == {1, 2, 3}                           # joins, removes and evictions
 
 
+@pytest.mark.parametrize("kinds", [_lib.EVENTS_REMOVE, _lib.EVENTS_JOIN,
+                                   _lib.EVENTS_REMOVE | _lib.EVENTS_EVICT])
+def test_event_kind_mask(kinds):
+    """params.events as a kind mask: only the selected kinds are recorded, all of them."""
+    sel = tuple(k for k in (1, 2, 3) if kinds >> k & 1)
+    n, ticks = 1200, 24
+    kw = dict(fanout=3, drop_pct=10, fail_mode=RANDOM, fail_tick=6, fail_ppm=30000, seed=29,
+              tremove=10)
+    orc = ScaleOracle(n, **kw)
+    with ScaleEngine(n, max_ticks=ticks, events=kinds, **kw) as eng:
+        for t in range(1, ticks + 1):
+            orc.step()
+            eng.step(1)
+            _check_tick(eng, orc, t, sel)
+    pkw = dict(view=48, fanout=3, inbox=5, drop_pct=10, fail_mode=RANDOM, fail_tick=6,
+               fail_ppm=30000, seed=29, tremove=10)
+    orc = PviewOracle(n, **pkw)
+    with PviewEngine(n, max_ticks=ticks, events=kinds, **pkw) as eng:
+        for t in range(1, ticks + 1):
+            orc.step()
+            eng.step(1)
+            _check_tick(eng, orc, t, sel)
+
+
 def test_event_ring_overflow_counts_lost():
-    """A ring smaller than one tick's events keeps cap records and counts the rest as lost."""
+    """A ring too small for the run: its 256 stripes (row % 256) keep event_cap / 256 records
+    each (rounded up), and every record beyond is counted as lost -- held + lost = all."""
     n, ticks = 400, 8                                   # ~40 crashes at t = 2, tremove 3
     with ScaleEngine(n, max_ticks=ticks, fanout=3, seed=5, fail_mode=RANDOM, fail_tick=2,
                      fail_ppm=100000, tremove=3, events=True, event_cap=100) as eng:
         eng.drain_events()
         eng.step(ticks)
+        total = sum(eng.digest(t)["joins"] + eng.digest(t)["removes"] for t in range(1, ticks + 1))
         rec, lost = eng.drain_events()
-        assert len(rec) == 100 and lost > 0
+        assert 0 < len(rec) <= 256 and lost > 0 and len(rec) + lost == total
         rec, lost = eng.drain_events()                  # the drain emptied the ring
         assert len(rec) == 0 and lost == 0
 
