@@ -25,7 +25,7 @@ class GspParams(ctypes.Structure):
                 ("msg_drop_prob", ctypes.c_double), ("step_rate", ctypes.c_double),
                 ("max_msg_size", c_int32), ("en_buff_size", c_int32),
                 ("total_running_time", c_int32), ("tremove", c_int32),
-                ("id_filter_limit", c_int32)]
+                ("id_filter_limit", c_int32), ("intro_list", c_int32)]
 
 
 class GspMemberView(ctypes.Structure):

@@ -214,6 +214,8 @@ int gsp_create(const gsp_params *p, int device, gsp_rng_mode rng, uint64_t seed,
                 "gsp_create: max_nnb=%d outside [1, %d]", p->max_nnb, kMaxNodes);
     GSP_REQUIRE(rng == GSP_RNG_GLIBC || rng == GSP_RNG_PHILOX, GSP_ERR_INVALID,
                 "gsp_create: unknown rng mode %d", int(rng));
+    GSP_REQUIRE(p->intro_list >= 0 && p->intro_list <= 16, GSP_ERR_INVALID,
+                "gsp_create: intro_list=%d outside [0, 16]", p->intro_list);
     *out = nullptr;
     int ndev = 0;
     GSP_HIP(hipGetDeviceCount(&ndev));
@@ -333,7 +335,7 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         int32_t njreq = 0;
         if (op == GSP_OP_LOOP || op == GSP_OP_CHECK) {
             for (const NetMsg &m : e->queue[node]) {
-                if (m.type == GSP_MSG_GOSSIP) {
+                if (m.type == GSP_MSG_GOSSIP || (m.type == GSP_MSG_JOINREP && e->p.intro_list > 0)) {
                     const int32_t s = m.src - 1;
                     // the payload is the sender's list at send time (MP1Node.cpp:357); the
                     // device reads it from the committed table, so it must be unchanged
@@ -385,6 +387,8 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     b.send_dst = e->send_dst.p; b.send_type = e->send_type.p; b.send_cnt = e->send_cnt.p;
     b.events = e->events.p; b.ev_count = e->counters.p; b.ev_cap = ev_cap;
     b.merges = e->merges.p;
+    b.intro_list = e->p.intro_list;
+    b.seed = e->seed;
 
     gsp::ExactSendDev s{};
     s.n_batch = n;

@@ -96,6 +96,33 @@ exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int
                     n_replies++;
                 } else {
                     in_group = 1;
+                    if (b.intro_list > 0 && valid && x != sc) {   // opt-in bounded introducer list
+                        const size_t srow = size_t(sc) * n;
+                        const int32_t cnt = tab.nlist[sc];
+                        const int32_t B = b.intro_list < cnt ? b.intro_list : cnt;
+                        int32_t ranks[16];
+                        int32_t nch = 0;
+                        for (int32_t i = 0; i < B; ++i)
+                            next_distinct_rank(draw_u31(kDomainJoin, b.seed, uint32_t(tick - 1), 0u,
+                                                        uint32_t(r), uint32_t(i)), cnt, i, ranks, nch);
+                        const int64_t kv = tab.key[srow + x];
+                        bool chosen = false;
+                        if (kv >= 0)
+                            for (int32_t i = 0; i < nch; ++i) chosen = chosen || ranks[i] == tab.rank[srow + x];
+                        // the GOSSIP payload rules (MP1Node.cpp:244-258), filter included
+                        if (chosen && x + 1 < id_filter_limit) {
+                            const int32_t hv = tab.hb[srow + x];
+                            const int32_t tv = tab.ts[srow + x];
+                            if (present) {
+                                if (hv > hb) { hb = hv; ts = tick; }
+                            } else if (x != r && tick - tv < tremove) {
+                                const int32_t p1 = tab.rank[srow + x] + 1;
+                                present = true; hb = hv; ts = tv;
+                                key = make_key(batch_seq, j, p1);
+                                push_event(b, pos, kEvJoin, x, (int64_t(j) << 20) | p1);
+                            }
+                        }
+                    }
                 }
             } else if (type == 3) {                // GOSSIP
                 merges += 1ull + uint64_t(tab.nlist[sc]);

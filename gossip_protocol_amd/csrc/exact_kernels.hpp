@@ -46,6 +46,8 @@ struct ExactBatchDev {
     int32_t *ev_count;                 // [1]
     int32_t ev_cap;
     unsigned long long *merges;        // [1]
+    int32_t intro_list;                // JOINREP payload bound (gsp_params.intro_list; 0 = off)
+    uint64_t seed;                     // Philox key of the introducer-list draws
 };
 
 // Send builder: assigns global draw indices in batch order, draws, applies the drop

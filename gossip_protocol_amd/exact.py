@@ -95,9 +95,11 @@ class Engine:
 
 
 def run_application(conf_path, seed, rng="glibc", out_dir=".", device=0, ticks=None,
-                    state_dump=True):
-    """Run one testcase the way the reference Application does; returns output paths."""
+                    state_dump=True, intro_list=0):
+    """Run one testcase the way the reference Application does; returns output paths.
+    intro_list: gsp_params.intro_list, the opt-in bounded introducer list (0 = reference)."""
     p = params_from_conf(conf_path)
+    p.intro_list = intro_list
     n = p.max_nnb
     T = p.total_running_time if ticks is None else ticks
     os.makedirs(out_dir, exist_ok=True)

@@ -81,6 +81,15 @@ typedef struct {
     int32_t total_running_time; /* TOTAL_RUNNING_TIME, 700 (Application.h:27)          */
     int32_t tremove;            /* TREMOVE, 20 (MP1Node.h:21)                          */
     int32_t id_filter_limit;    /* payload filter id < limit, 10 (MP1Node.cpp:245)     */
+    int32_t intro_list;         /* opt-in protocol variant, 0 = the reference: the JOINREP
+                                   carries the introducer's whole list and its receiver ignores
+                                   it (MP1Node.cpp:221-233).  B = 1..16: the joiner merges B
+                                   entries of the introducer's list, chosen by sequential
+                                   distinct Philox ranks over list order (Philox(JOIN; t - 1,
+                                   0, joiner index, i), t = the handling tick), with the GOSSIP
+                                   payload rules (MP1Node.cpp:244-258, id filter included); the
+                                   list is the introducer's as of the end of the tick it
+                                   replied (the snapshot its GOSSIPs of that tick carry)      */
 } gsp_params;
 
 int gsp_params_default(gsp_params *out);

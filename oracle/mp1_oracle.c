@@ -127,6 +127,9 @@ void gsp_oracle_mp1_set_queue_trace(const char *path) {
     if (path) snprintf(g_trace_path, sizeof g_trace_path, "%s", path);
 }
 int64_t gsp_oracle_mp1_buffer_full_rejects(void) { return g_buffer_full_rejects; }
+/* opt-in bounded introducer list (gsp_params.intro_list; 0 = the reference) */
+static int g_intro_list;
+void gsp_oracle_mp1_set_intro_list(int b) { g_intro_list = b; }
 
 /* ---------------- EmulNet (EmulNet.cpp) ---------------- */
 static void en_send(sim_t *s, int src_node, int dst_id, int type, const entry_t *pl, int npl) {
@@ -193,6 +196,35 @@ static void handle(sim_t *s, int node, msg_t *m) {       /* recvCallBack, MP1Nod
     } else if (m->type == M_JOINREP) {
         add_from_header(s, node, m->src);
         nd->in_group = 1;
+        if (g_intro_list > 0) {
+            /* variant: merge B entries of the introducer's list as of the end of the tick it
+             * replied -- its current list, since phase P runs it last (Application.cpp:138) --
+             * at sequential distinct Philox ranks, with the GOSSIP payload rules */
+            const node_t *in = &s->nodes[m->src - 1];
+            const int cnt = in->nlist, b = g_intro_list < cnt ? g_intro_list : cnt;
+            int ranks[16], nch = 0;
+            for (int i = 0; i < b; ++i) {
+                int rk = (int)(gsp_philox_u31(GSP_DOMAIN_JOIN, s->seed, (uint32_t)(s->t - 1), 0,
+                                              (uint32_t)node, (uint32_t)i) % (uint32_t)(cnt - i));
+                int pos = 0;
+                while (pos < nch && rk >= ranks[pos]) { rk++; pos++; }
+                memmove(&ranks[pos + 1], &ranks[pos], sizeof(int) * (size_t)(nch - pos));
+                ranks[pos] = rk;
+                nch++;
+            }
+            entry_t pick[16];
+            for (int i = 0; i < nch; ++i) pick[i] = in->list[ranks[i]];   /* ascending position */
+            for (int i = 0; i < nch; ++i) {
+                const entry_t *v = &pick[i];
+                if (!(v->id >= 0 && v->id < ID_FILTER_LIMIT)) continue;
+                entry_t *x = find(nd, v->id);
+                if (x) {
+                    if (v->hb > x->hb) { x->hb = v->hb; x->ts = s->t; }
+                } else {
+                    add_from_entry(s, node, v);
+                }
+            }
+        }
     } else if (m->type == M_GOSSIP) {
         entry_t *e = find(nd, m->src);
         if (e) { e->hb += 1; e->ts = s->t; }

@@ -98,6 +98,7 @@ def load_oracle():
                                          ctypes.c_int] + [ctypes.c_char_p] * 4
         L.gsp_oracle_mp1_run.restype = ctypes.c_int
         L.gsp_oracle_mp1_buffer_full_rejects.restype = ctypes.c_int64
+        L.gsp_oracle_mp1_set_intro_list.argtypes = [ctypes.c_int]
         L.gsp_glibc_stream.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32),
                                        ctypes.c_int64]
         L.gsp_scale_oracle_create.argtypes = [ctypes.POINTER(ScaleCfg)]
@@ -198,12 +199,18 @@ def outputs_for_big(paths):
     return out
 
 
-def run_oracle_mp1(conf, seed, mode, out_dir, ticks=700):
+def run_oracle_mp1(conf, seed, mode, out_dir, ticks=700, intro_list=0):
+    """intro_list: the exact engine's opt-in bounded introducer list (0 = the reference)."""
     L = load_oracle()
     os.makedirs(out_dir, exist_ok=True)
     p = lambda x: os.path.join(out_dir, x).encode()
-    rc = L.gsp_oracle_mp1_run(conf_path(conf).encode(), seed, MODES.index(mode), ticks,
-                              p("dbg.log"), p("msgcount.log"), p("state.txt"), p("stdout.txt"))
+    L.gsp_oracle_mp1_set_intro_list(intro_list)
+    try:
+        rc = L.gsp_oracle_mp1_run(conf_path(conf).encode(), seed, MODES.index(mode), ticks,
+                                  p("dbg.log"), p("msgcount.log"), p("state.txt"),
+                                  p("stdout.txt"))
+    finally:
+        L.gsp_oracle_mp1_set_intro_list(0)
     assert rc == 0, rc
     return {f: os.path.join(out_dir, f) for f in FILES}
 

@@ -127,3 +127,5 @@ def test_bench_two_ranks_gloo():
     assert ev["first_detection_latency_ticks"] == {"min": 1, "mean": 10.5, "max": 20}
     assert ev["full_detection_latency_ticks"] == {"min": 3, "mean": 12.0, "max": 21}
     assert ev["kernel_overhead_frac"] == 0.0
+    pe = pv["events"]                                 # the partial view's removes-only run
+    assert pe["kinds"] == 4 and pe["crashed_nodes_detected"] == 2 and pe["kernel_overhead_frac"] == 0.0
