@@ -167,13 +167,16 @@ def pview_cpu_baseline(budget_s=10.0):
             "sample": "oracle/pview_oracle.c, n=5000, V=256, %d ticks in %.1f s" % (ticks, el)}
 
 
-def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1):
+def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1, events=0):
     """Config 5 on `world` GPUs (row shards).  Returns the rank-0 summary (None elsewhere).
     Algorithmic bytes per node-round: own view read + write (2 * V * 8) + one sender view per
-    merged message (V * 8) + 4 B per CSR entry."""
+    merged message (V * 8) + 4 B per CSR entry.  events: a kind mask (gsp_pview_params.events);
+    the summary is then the event one (event_summary) with the kernel time."""
     import torch
     from gossip_protocol_amd.pview import PviewEngine
     kw = dict(PV_KW, max_ticks=warmup + steps)
+    if events:
+        kw.update(events=events, event_cap=EVENT_CAP)
     if dist is not None:
         from gossip_protocol_amd.dist import make_pview_rank_engine
         eng = make_pview_rank_engine(nodes, local, **kw)
@@ -181,6 +184,8 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         eng = PviewEngine(nodes, device=local, group=group, **kw)
     eng.step(warmup)
     eng.sync()
+    if events:
+        eng.drain_events()
     p0 = eng.perf()
     if dist is not None:
         dist.barrier()
@@ -206,6 +211,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     xch_ms = (p1["csr_ms"] - p0["csr_ms"]) / launches
     bytes_per_launch = ((2.0 * rounds + delivered) * V * 8.0 + csr * 4.0) / steps
     xgmi = (p1["xgmi_bytes"] - p0["xgmi_bytes"]) / steps
+    ev = event_summary(eng, nodes, warmup + steps, dist) if events else None
     eng.close()
     if dist is not None:
         t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device=_dev())
@@ -217,6 +223,9 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         rounds, merges, bytes_per_launch, xgmi = (x.item() for x in u)
         if dist.get_rank() != 0:
             return None
+    if events:
+        ev.update({"kinds": events, "kernel_ms": kern_ms, "value_events_on": rounds / el})
+        return ev
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     peak = PEAK_HBM_GBS * world
     out = {
@@ -270,7 +279,7 @@ def _pview_valu(nodes, world, kern_ms):
             "frac_of_2cycle_issue": per_cycle * 2.0, "clock_ghz": 2.4}
 
 
-EVENT_CAP = 1 << 26          # records per shard (512 MB): config 3's ~42.5 M removes fit
+EVENT_CAP = 1 << 27          # records per shard (1 GB): config 3 records 70.7 M joins + removes
 
 
 def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=False):
@@ -511,6 +520,18 @@ def main(argv=None):
     if not args.no_pview:
         item("pview", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world,
                                         local, dist, not args.no_cpu_baseline))
+    if not args.no_pview and not args.no_events:
+        # the partial view records removes only: its joins and evictions are ~8e8 records per
+        # tick at config 5 (6.7 GB, more than the tick's state traffic; scripts/events_cost.py)
+        def _pv_events():
+            r = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
+                          False, events=4)
+            if r is not None and out is not None and isinstance(out.get("pview"), dict) \
+                    and "roofline" in out["pview"]:
+                k0 = out["pview"]["roofline"]["kernel_ms"]
+                r.update(kernel_ms_events_off=k0, kernel_overhead_frac=r["kernel_ms"] / k0 - 1.0)
+            return r
+        item("pview", _pv_events, "events")
     if world > 1 and not args.no_262k:
         # BASELINE config 4: 262,144 nodes full view over the same column shards (its 137 GB
         # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)

@@ -188,11 +188,36 @@ struct RowOut {
     uint64_t hsum;
 };
 
+// The bounded introducer list (block-uniform): bit q of m = rank q of node 0's gossiped members
+// is carried -- B sequential distinct Philox ranks (next_distinct_rank, philox.hpp) kept as a
+// 256-bit mask instead of a sorted array, so nothing is indexed dynamically (no scratch).
+__device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r, int32_t cnt,
+                                     int32_t B, uint64_t (&m)[4]) {
+    m[0] = m[1] = m[2] = m[3] = 0ull;
+    for (int32_t i = 0; i < B; ++i) {
+        int32_t rk = int32_t(draw_u31(kDomainJoin, seed, t_send, 0u, r, uint32_t(i)) % uint32_t(cnt - i));
+        bool done = false;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {                    // the rk-th rank not chosen yet
+            const int32_t zeros = 64 - __popcll(m[w]);
+            if (!done && rk < zeros) {
+                uint64_t z = ~m[w];
+                for (int32_t q = 0; q < rk; ++q) z &= z - 1;
+                m[w] |= z & (~z + 1);
+                done = true;
+            }
+            if (!done) rk -= zeros;
+        }
+    }
+}
+
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
-// jrep: message 1 is a JOINREP (its payload: node 0's view cut to the bounded introducer
-// list); pcol / pok: the SWIM probe of t - 1 (target id or kNoId, answered).
-template <int kBlocks>
+// kExt: the protocol extensions are compiled in -- TFAIL payload filter, JOINREP (jrep:
+// message 1 is a JOINREP whose payload is node 0's view cut to the bounded introducer list),
+// SWIM (pcol / pok: the probe of t - 1, target id or kNoId, answered) and the event stream;
+// the plain protocol (config 5) runs the kernel without them.
+template <int kBlocks, bool kExt>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
                                              int32_t k, uint64_t ent0, int32_t my_slot,
                                              const uint32_t (&ssrc)[kPvMaxInbox], bool jrep,
@@ -226,25 +251,19 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             const uint64_t *row = (m == 1 && jrep) ? a.intro
                                   : sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
             ent[m] = __builtin_nontemporal_load(row + tid);
-            if (!gossiped(ent[m])) ent[m] = kPvEmpty;
+            if (kExt && !gossiped(ent[m])) ent[m] = kPvEmpty;
         }
     }
-    if constexpr (kBlocks > 1) if (jrep) {   // block-uniform: rank node 0's gossiped members
+    if constexpr (kBlocks > 1 && kExt) if (jrep) {   // block-uniform: node 0's gossiped members
         const bool g = ent[1] != kPvEmpty;
         uint32_t cnt0 = 0;
         const uint32_t rank = block_scan(g ? 1u : 0u, &cnt0, sh.keys[1]);   // keys[1] is free here
         const int32_t B = a.intro_list < int32_t(cnt0) ? a.intro_list : int32_t(cnt0);
-        int32_t ranks[kMaxIntro];
-        int32_t nch = 0;
-        bool chosen = false;
-        for (int32_t i = 0; i < B; ++i) {
-            const int32_t rk = next_distinct_rank(
-                draw_u31(kDomainJoin, a.seed, t - 1u, 0u, uint32_t(r), uint32_t(i)), int32_t(cnt0), i,
-                ranks, nch);
-            (void)rk;
-        }
-        for (int32_t i = 0; i < nch; ++i) chosen = chosen || (g && uint32_t(ranks[i]) == rank);
-        if (!chosen) ent[1] = kPvEmpty;
+        uint64_t cm[4];
+        pv_intro_mask(a.seed, t - 1u, uint32_t(r), int32_t(cnt0), B, cm);
+        const uint32_t w = rank >> 6;
+        const uint64_t word = w == 0 ? cm[0] : w == 1 ? cm[1] : w == 2 ? cm[2] : cm[3];
+        if (!(g && ((word >> (rank & 63u)) & 1ull))) ent[1] = kPvEmpty;
     }
     // A TFAIL- or introducer-filtered payload has holes: its keys are compacted to the front
     // of the block (the tree merges sorted blocks).  Block-uniform; one scan per message.
@@ -253,7 +272,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
         kpos[m] = tid;
-        if (m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
+        if (kExt && m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
             const bool ok = ent[m] != kPvEmpty;
             uint32_t cnt = 0;
             const uint32_t pos = block_scan(ok ? 1u : 0u, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
@@ -266,8 +285,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     for (int m = 0; m < kBlocks; ++m) {
         const bool ok = ent[m] != kPvEmpty;
         merged += (m >= 1 && ok) ? 1u : 0u;
-        if ((kpad >> m) & 1u) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted block's tail
-        if (kpos[m] >= 0)
+        if (kExt && ((kpad >> m) & 1u)) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted tail
+        if (!kExt || kpos[m] >= 0)
             sh.keys[0][m * kSlots + kpos[m]] =
                 ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
         sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
@@ -390,12 +409,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (!aown) continue;
         if (ajs && !adone) av = pv_event(av, t5);
         if (x == uint32_t(r) || !av) continue;                  // never list yourself
-        if (x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
-        if (!ae0) { joins++; hsum += pv_hash(S_join, x); jmask |= 1u << e; }
+        if (kExt && x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
+        if (!ae0) { joins++; hsum += pv_hash(S_join, x); if (kExt) jmask |= 1u << e; }
         if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
             hsum += pv_hash(S_remove, x);
-            rmask |= 1u << e;
+            if (kExt) rmask |= 1u << e;
             continue;
         }
         res[e] = av;
@@ -421,7 +440,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
     }
 
-    if (a.ev.buf) {                                      // event stream: joins and removes
+    if (kExt && a.ev.buf) {                              // event stream: joins and removes
         if (!(a.ev.kinds & GSP_EVENTS_JOIN)) jmask = 0;
         if (!(a.ev.kinds & GSP_EVENTS_REMOVE)) rmask = 0;
         const uint32_t amask = (a.ev.kinds & GSP_EVENTS_JOIN) ? adopt : 0u;
@@ -590,7 +609,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
-        const bool ev_on = a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
+        const bool ev_on = kExt && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
         if (ev_on) {
             const int32_t tk = int32_t(need2) - int32_t(tie_before);
             const uint32_t kept = nk + uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
@@ -682,6 +701,7 @@ __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) 
 
 // One non-init row: the own view slot and the receipt record are requested first (their
 // latencies overlap), then merge, ops, eviction, view write and digest record.
+template <bool kExt>
 __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int32_t lr) {
     const int32_t tid = threadIdx.x, lane = tid & 63;
     const int32_t r = a.row0 + lr;
@@ -701,7 +721,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     const int32_t info = __builtin_amdgcn_readfirstlane(info_v);
     const int32_t k = info & 7, k_all = info >> 3;
     // a JOINREP (sender kJoinRepSrc) sorts first; its sender event is node 0's
-    const bool jrep = k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
+    const bool jrep = kExt && k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
     uint32_t ssrc[kPvMaxInbox];
 #pragma unroll
     for (int jj = 0; jj < kPvMaxInbox; ++jj)
@@ -711,7 +731,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     // the swim paths survived its drop draw (paths sent at t - 1)
     uint32_t pcol = kNoId;
     bool pok = false;
-    if (a.swim > 0) {
+    if (kExt && a.swim > 0) {
         const int32_t p = __builtin_amdgcn_readfirstlane(a.ping[lr]);
         if (p >= 0) {
             pcol = uint32_t(p);
@@ -723,14 +743,14 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     }
     pm.mark(0);
     // one variant per key count (own view + k sender views)
-    if (k == 0) pv_merge_row<1>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 1) pv_merge_row<2>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 2) pv_merge_row<3>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 3) pv_merge_row<4>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 4) pv_merge_row<5>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 5) pv_merge_row<6>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 6) pv_merge_row<7>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else pv_merge_row<8>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    if (k == 0) pv_merge_row<1, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 1) pv_merge_row<2, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 2) pv_merge_row<3, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 3) pv_merge_row<4, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 4) pv_merge_row<5, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 5) pv_merge_row<6, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else if (k == 6) pv_merge_row<7, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+    else pv_merge_row<8, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
     pm.mark(5);
     pv_finish(a, sh, lr, k, k_all, false, ro);
     pm.mark(6);
@@ -787,10 +807,10 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
 // workgroup: a software-pipelined variant (the next row's record, own view and first sender
 // views requested while the current row merged, two rows per workgroup) measured 4-8 % slower
 // -- other resident rows already hide the HBM round trips.
-template <int kWaves>
+template <int kWaves, bool kExt>
 __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared sh;
-    pv_row(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
+    pv_row<kExt>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
 }
 
 // One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
@@ -1013,8 +1033,15 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     if (!pv_args_ok(a)) return hipErrorInvalidValue;
     if (a.rows == 0) return hipSuccess;
     const dim3 g(unsigned(a.rows)), blk(kPvBlock);
-    if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8>), g, blk, 0, st, a);
-    else hipLaunchKernelGGL((pview_tick_kernel<7>), g, blk, 0, st, a);
+    // the protocol extensions in use (TFAIL, SWIM, joins, events) select the kExt kernel
+    const bool ext = a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr || a.ev.buf != nullptr;
+    if (ext) {
+        if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8, true>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((pview_tick_kernel<7, true>), g, blk, 0, st, a);
+    } else {
+        if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8, false>), g, blk, 0, st, a);
+        else hipLaunchKernelGGL((pview_tick_kernel<7, false>), g, blk, 0, st, a);
+    }
     launch_send_and_digest(a, st);
     return hipGetLastError();
 }
