@@ -317,13 +317,45 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 sb = rest - s < s ? (rest > s ? rest - s : 0) : s;
             }
             int32_t lo = o > sb ? o - sb : 0, hi = o < sa ? o : sa;
+#if GSP_PV_CORANK4
+            while (lo < hi) {                                  // co-rank of output o, 4-ary:
+                const int32_t len = hi - lo;                   // three independent probes a step
+                const int32_t m1 = lo + (len >> 2), m2 = lo + (len >> 1), m3 = lo + ((3 * len) >> 2);
+                const bool f1 = A[m1] < B[o - m1 - 1], f2 = A[m2] < B[o - m2 - 1],
+                           f3 = A[m3] < B[o - m3 - 1];
+                if (f3) lo = m3 + 1;
+                else if (f2) { lo = m2 + 1; hi = m3; }
+                else if (f1) { lo = m1 + 1; hi = m2; }
+                else hi = m1;
+            }
+#else
             while (lo < hi) {                                  // co-rank of output o
                 const int32_t mid = (lo + hi) >> 1;
                 if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
             }
+#endif
             int32_t i = lo, j = o - lo;
-            uint32_t va = i < sa ? A[i] : kKeyMax, vb = j < sb ? B[j] : kKeyMax;
             uint32_t outk[Qt];
+#if GSP_PV_TREE_WIN
+            // the next Qt keys of each side (independent loads), then the Qt smallest of the
+            // two windows: min(A[e], B[Qt-1-e]) is bitonic, and a half-cleaner network sorts it
+#pragma unroll
+            for (int e = 0; e < Qt; ++e) {
+                const uint32_t wa = i + e < sa ? A[i + e] : kKeyMax;
+                const uint32_t wb = j + (Qt - 1 - e) < sb ? B[j + (Qt - 1 - e)] : kKeyMax;
+                outk[e] = wa < wb ? wa : wb;
+            }
+#pragma unroll
+            for (int d = Qt / 2; d >= 1; d >>= 1)
+#pragma unroll
+                for (int e = 0; e < Qt; ++e)
+                    if ((e & d) == 0) {
+                        const uint32_t x = outk[e], y = outk[e + d];
+                        outk[e] = x < y ? x : y;
+                        outk[e + d] = x < y ? y : x;
+                    }
+#else
+            uint32_t va = i < sa ? A[i] : kKeyMax, vb = j < sb ? B[j] : kKeyMax;
 #pragma unroll
             for (int e = 0; e < Qt; ++e) {
                 const bool ta = va <= vb;                      // equal only for padding
@@ -335,6 +367,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 va = ta ? nv : va;
                 vb = ta ? vb : nv;
             }
+#endif
             lds_store<Qt>(Y + begt, outk);
         }
         __syncthreads();

@@ -605,6 +605,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
         }
     }
     if (kSlice) return;
+#if GSP_SCALE_NOSEND   // measurement only: the merge without the send step (wrong protocol)
+    if (!kInit) { if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1; return; }
+#endif
 
     // send: wave 0 picks min(F, live) distinct members by Philox rank-select
     if (wave == 0) {
