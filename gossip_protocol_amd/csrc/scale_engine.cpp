@@ -64,6 +64,10 @@ struct gsp_scale {
     int32_t shards = 1;        // G: column shards in the whole job
     int32_t rank = 0;          // first shard index held by this engine
     bool sliced = false;       // column layout (G > 1)
+    bool shared = false;       // column layout, every shard in this process on one device (an
+                               // in-process group): the shards share shard 0's CSR, counts,
+                               // picks and sends, so the tick has no exchange at all -- G
+                               // column tiles of one GPU's job (DESIGN.md "Column tiles")
     bool rowmode = false;      // row layout (G > 1): sender rows move between shards
     int64_t pair_cap = 0, msg_cap = 0;
     int32_t *h_cnt = nullptr, *h_recv = nullptr;   // pinned exchange counts (row layout)
@@ -128,19 +132,24 @@ struct gsp_scale {
         // row layout's shard 0 broadcast
         a.intro = (rowmode && sh.row0 != 0) ? sh.intro_buf.p : sh.table[(t + 1) & 1].p;
         a.intro_list = p.policy.intro_list;
-        a.intro_cnt = sliced ? sh.cnt_all.p : nullptr;
+        const Shard &s0 = local[0];
+        // shared: cnt_all[tick parity][G][n], so this tick's slice counts never overwrite the
+        // tick-(t - 1) counts another shard's JOINREP still reads
+        const size_t gn = size_t(shards) * size_t(p.n);
+        a.intro_cnt = sliced ? (shared ? s0.cnt_all.p + size_t((t + 1) & 1) * gn : sh.cnt_all.p) : nullptr;
         a.shards = shards;
         a.shard = sh.g;
         a.own_hb = sh.own_hb.p;
-        a.cnt_prev = sh.cnt_total[(t + 1) & 1].p;
-        a.cnt_cur = sliced ? sh.cnt_slice.p : sh.cnt_total[t & 1].p;
-        a.off = sh.off.p;
-        a.csr_src = sh.csr_src.p;
+        a.cnt_prev = (shared ? s0 : sh).cnt_total[(t + 1) & 1].p;
+        a.cnt_cur = shared ? s0.cnt_all.p + size_t(t & 1) * gn + size_t(sh.g) * size_t(p.n)
+                  : sliced ? sh.cnt_slice.p : sh.cnt_total[t & 1].p;
+        a.off = (shared ? s0 : sh).off.p;
+        a.csr_src = (shared ? s0 : sh).csr_src.p;
         a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
         a.out_dst = sh.out_dst.p;
         a.deg = sh.deg.p;
-        a.ping = sh.ping.p;
-        a.bitmap = sh.bitmap.p;
+        a.ping = (shared ? s0 : sh).ping.p;
+        a.bitmap = shared ? s0.bitmap.p + size_t(sh.g) * size_t(p.n) * size_t(stride / 8) : sh.bitmap.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
         a.max_segment = max_segment;
@@ -161,10 +170,12 @@ struct gsp_scale {
         r.fail_tick = sh.fail_tick.p;
         r.start_tick = joins ? sh.start_tick.p : nullptr;
         r.drop_pct = gsp::drop_at(p.policy, p.drop_pct, t);
-        r.cnt_all = sh.cnt_all.p;
+        r.cnt_all = shared ? local[0].cnt_all.p + size_t(t & 1) * size_t(shards) * size_t(p.n) : sh.cnt_all.p;
         r.cnt_total = sh.cnt_total[t & 1].p;
         r.bitmap = sh.bitmap.p;
         r.picks = sh.picks.p;
+        r.tiled = shared ? 1 : 0;       // one launch resolves every shard's ranks
+        r.tile_bytes = int64_t(p.n) * (stride / 8);
         r.swim = p.swim;
         r.ping = sh.ping.p;
         r.out_dst = sh.out_dst.p;
@@ -230,11 +241,12 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     GSP_HIP(sh.csr_src.alloc(size_t(n) * s->p.fanout));
     GSP_HIP(sh.err.alloc(1));
     GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
-    if (s->sliced) {
+    if (s->sliced && (!s->shared || &sh == &s->local[0])) {
         GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
-        GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards));
+        GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards * (s->shared ? 2 : 1)));
         GSP_HIP(sh.picks.alloc(size_t(n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0))));
-        GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8)));
+        // shared: every shard's bitmap, one region per shard (the resolve reads them all)
+        GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8) * (s->shared ? size_t(s->shards) : 1)));
     }
     if (s->rowmode)
         GSP_HIP(sh.x.alloc(s->shards, s->pair_cap, s->msg_cap, int32_t(s->stride / 4),
@@ -267,6 +279,7 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
 // all-gather of every shard's per-row slice counts into every shard's cnt_all[G][n]
 int exchange_counts(gsp_scale *s) {
     const size_t n = size_t(s->p.n);
+    if (s->shared) return GSP_OK;         // the shards wrote shard 0's cnt_all directly
     if (s->comm) {
         Shard &sh = s->local[0];
         GSP_NCCL(ncclAllGather(sh.cnt_slice.p, sh.cnt_all.p, n, ncclInt32, s->comm, s->st));
@@ -298,6 +311,11 @@ int exchange_picks(gsp_scale *s) {
 
 // message generation for tick t (columns: after the slices are merged)
 int resolve_sends(gsp_scale *s, int32_t t) {
+    if (s->shared) {                     // one resolve over every shard's ranks, one finalize
+        GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(s->local[0], t), s->st));
+        GSP_HIP(gsp::launch_scale_finalize(s->resolve_args(s->local[0], t), s->st));
+        return GSP_OK;
+    }
     // egress per shard of ring collectives: all-gather (G-1)/G of G*n*4 B, all-reduce
     // 2 (G-1)/G of n*f*4 B
     const double G = double(s->shards), n = double(s->p.n);
@@ -374,6 +392,7 @@ int join_sends(gsp_scale *s, int32_t t) {
     const int64_t cnt = s->plan.count(t + 1);
     if (!s->joins || cnt == 0) return GSP_OK;
     for (Shard &sh : s->local) {
+        if (s->shared && &sh != &s->local[0]) continue;   // one CSR (shard 0's deg)
         gsp::JoinSendArgs j{};
         j.joiners = sh.joiners.p + s->plan.first(t + 1);
         j.count = int32_t(cnt);
@@ -414,11 +433,13 @@ int join_sends(gsp_scale *s, int32_t t) {
 int join_scatter(gsp_scale *s, int32_t t) {
     const int64_t cnt = s->plan.count(t);
     if (!s->joins || cnt == 0) return GSP_OK;
-    for (Shard &sh : s->local)
+    for (Shard &sh : s->local) {
+        if (s->shared && &sh != &s->local[0]) continue;
         GSP_HIP(gsp::launch_join_scatter(sh.joiners.p + s->plan.first(t), sh.join_ok.p + s->plan.first(t),
                                          int32_t(cnt), s->rowmode ? sh.row0 : 0,
                                          s->rowmode ? sh.rows : s->p.n, sh.off.p, sh.fill.p, sh.csr_src.p,
                                          s->rowmode ? sh.x.csr_slot.p : nullptr, s->st));
+    }
     return GSP_OK;
 }
 
@@ -461,6 +482,8 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     // a communicator always runs the sharded protocol (with one rank it exercises RCCL alone)
     const bool sharded = shards > 1 || nccl_id != nullptr;
     s->sliced = sharded && layout == GSP_SHARD_COLUMNS;
+    s->shared = s->sliced && nccl_id == nullptr && local_shards > 1 && local_shards == shards;
+    if (const char *sx = std::getenv("GSP_SCALE_SHARED")) s->shared = s->shared && std::atoi(sx) != 0;
     s->rowmode = sharded && layout == GSP_SHARD_ROWS;
     const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
@@ -601,6 +624,7 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
             if (int rc = exchange_rows(s, t - 1)) return rc;
         } else {
             for (Shard &sh : s->local) {
+                if (s->shared && &sh != &s->local[0]) continue;   // one CSR for every shard
                 GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
                 GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
                 GSP_HIP(gsp::launch_scatter(sh.out_dst.p, slots, s->p.fanout, 0, sh.off.p, sh.fill.p,

@@ -675,9 +675,28 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
     const int32_t cnt = int32_t(total);
     const int32_t keff = F < cnt ? F : cnt;
     const int32_t per = int32_t(a.stride >> 5) >> 6;
-    const uint32_t *bm = reinterpret_cast<const uint32_t *>(a.bitmap + int64_t(s) * (a.stride >> 3));
-    bool have_counts = false;
+    // the bitmap of shard g's slice of row s, and its per-lane popcounts / prefix (cached for
+    // the last shard used: a sender's picks fall into few shards' slices)
+    const uint32_t *bm = nullptr;
+    int32_t bm_g = -1;
     uint32_t lane_cnt = 0, pre = 0;
+    auto resolve = [&](uint32_t rk) -> int32_t {        // wave-uniform rank -> column or -1
+        const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
+        const int32_t g = __builtin_ffsll(own) - 1;
+        if (g != a.shard && !a.tiled) return -1;        // another shard resolves it
+        if (g != bm_g) {
+            bm = reinterpret_cast<const uint32_t *>(a.bitmap + (a.tiled ? int64_t(g) * a.tile_bytes : 0) +
+                                                    int64_t(s) * (a.stride >> 3));
+            lane_cnt = 0;
+            for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);
+            uint32_t tot = 0;
+            pre = wave_excl_prefix(lane_cnt, lane, &tot);
+            bm_g = g;
+        }
+        const uint32_t local = rk - __shfl(cpre, g, 64);
+        const int32_t col = wave_select([&](int32_t w) { return bm[w]; }, per, lane_cnt, pre, local, lane);
+        return int32_t(int64_t(g) * a.stride + col);
+    };
     int32_t chosen[16];
     int32_t nch = 0;
     for (int32_t kk = 0; kk < F; ++kk) {
@@ -685,21 +704,7 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
         if (kk < keff) {
             const uint32_t u = draw_u31(kDomainPeer, a.seed, uint32_t(a.tick), uint32_t(s),
                                         uint32_t(kk), 0u);
-            const uint32_t rk = uint32_t(next_distinct_rank(u, cnt, kk, chosen, nch));
-            const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
-            const int32_t g = __builtin_ffsll(own) - 1;
-            if (g == a.shard) {
-                if (!have_counts) {
-                    for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);
-                    uint32_t tot = 0;
-                    pre = wave_excl_prefix(lane_cnt, lane, &tot);
-                    have_counts = true;
-                }
-                const uint32_t local = rk - __shfl(cpre, g, 64);
-                const int32_t col = wave_select([&](int32_t w) { return bm[w]; }, per, lane_cnt, pre,
-                                                local, lane);
-                pick = int32_t(int64_t(a.shard) * a.stride + col);
-            }
+            pick = resolve(uint32_t(next_distinct_rank(u, cnt, kk, chosen, nch)));
         }
         if (lane == 0) a.picks[int64_t(s) * W + kk] = pick;
     }
@@ -707,21 +712,7 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
         int32_t pick = -1;
         if (cnt > 0) {
             const uint32_t u = draw_u31(kDomainPing, a.seed, uint32_t(a.tick), uint32_t(s), 0u, 0x100u);
-            const uint32_t rk = u % uint32_t(cnt);
-            const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
-            const int32_t g = __builtin_ffsll(own) - 1;
-            if (g == a.shard) {
-                if (!have_counts) {
-                    for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);
-                    uint32_t tot = 0;
-                    pre = wave_excl_prefix(lane_cnt, lane, &tot);
-                    have_counts = true;
-                }
-                const uint32_t local = rk - __shfl(cpre, g, 64);
-                const int32_t col = wave_select([&](int32_t w) { return bm[w]; }, per, lane_cnt, pre,
-                                                local, lane);
-                pick = int32_t(int64_t(a.shard) * a.stride + col);
-            }
+            pick = resolve(u % uint32_t(cnt));
         }
         if (lane == 0) a.picks[int64_t(s) * W + F] = pick;
     }
