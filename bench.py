@@ -280,9 +280,11 @@ def _pview_valu(nodes, world, kern_ms):
 
 
 EVENT_CAP = 1 << 27          # records per shard (1 GB): config 3 records 70.7 M joins + removes
+TILES = 8                    # one GPU: config 3 as 8 column tiles of 8,192 columns (DESIGN.md
+                             # "Column tiles": 6.6 vs 8.0 ms per tick for the fused row kernel)
 
 
-def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=False):
+def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=False, tiles=None):
     """Full-view workload (config 3 rules) on `world` GPUs: one GPU fused, or column / row
     shards.  Returns job totals (time and kernel time are the slowest rank's).  events: the
     tick kernels also append every join / remove record to the device ring (drained after
@@ -297,7 +299,9 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
         from gossip_protocol_amd.dist import make_rank_engine
         eng = make_rank_engine(nodes, local, **kw)
     else:
-        eng = ScaleEngine(nodes, device=local, **kw)
+        if tiles is None:
+            tiles = TILES if nodes % (2048 * TILES) == 0 else 1
+        eng = ScaleEngine(nodes, device=local, group=tiles, **kw)
     eng.step(warmup)
     eng.sync()
     if events:
@@ -321,7 +325,7 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
         rounds += d["node_rounds"]
         merges += d["merges"]
         delivered += d["delivered"]
-    stride = eng.layout()[2]
+    shards_total, _, stride = eng.layout()
     launches = max(perf1["merge_launches"] - perf0["merge_launches"], 1)
     kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / launches
     csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / launches
@@ -342,11 +346,11 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
     # (2-byte entries), one 4-byte CSR entry per message; column shards stream their slice
     # (stride columns) of each such row, so the job moves `world` slices; row shards stream
     # whole rows (stride = full width) of their own receivers only
-    slices = world if layout == "columns" else 1
+    slices = shards_total if layout == "columns" else 1
     bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
     return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
             "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout,
-            "events": ev}
+            "events": ev, "tiles": shards_total if dist is None else 1}
 
 
 def event_summary(eng, nodes, last_tick, dist):
@@ -401,7 +405,9 @@ def summarize_full(r, nodes, steps, world):
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if nodes == N_NODES and world == 1 and os.path.exists(prof):
         try:
-            traffic = json.load(open(prof)).get("bytes_per_launch")
+            t = json.load(open(prof))
+            if t.get("launches_per_tick", 1) == r["tiles"]:
+                traffic = t.get("bytes_per_tick", t.get("bytes_per_launch"))
         except Exception:
             traffic = None
     cfg = "config3" if nodes == N_NODES else "config4" if nodes == 262144 else "full view"
@@ -413,12 +419,13 @@ def summarize_full(r, nodes, steps, world):
         "config": {"workload": "%s: %d nodes full view, fanout %d, 1%% random crash at t=%d, "
                                "no drops" % (cfg, nodes, FANOUT, FAIL_TICK),
                    "nodes": nodes, "view": nodes, "fanout": FANOUT, "entry_bytes": 2,
-                   "parallelism": "%s%d" % (r["layout"], world) if world > 1 else "1gpu"},
+                   "parallelism": "%s%d" % (r["layout"], world) if world > 1 else
+                   "1gpu" if r["tiles"] == 1 else "1gpu-%dtiles" % r["tiles"]},
         "merges_per_s": r["merges"] / r["el"],
         "xgmi_bytes_per_tick": r["xgmi_tick"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
-                     "kernel_ms": r["kern_ms"],
+                     "kernel_ms": r["kern_ms"], "launches_per_tick": r["tiles"],
                      ("exchange_csr_ms" if r["layout"] == "rows" else "csr_ms"): r["csr_ms"],
                      "algorithmic_bytes_per_launch": r["bytes_per_launch"]},
     }

@@ -31,7 +31,7 @@ step pv_fetch 200 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pv_fetch" -o run --output-
 step pv_write 200 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pv_write" -o run --output-format csv -- python3 $PVB
 step pv_sq 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS -d "$OUT/pv_sq" -o run --output-format csv -- python3 $PVB
 cd "$GRAFT_REPO_ROOT"
-python3 scripts/pmc_traffic.py $(ls "$OUT"/pmc_fetch/*counter_collection.csv) $(ls "$OUT"/pmc_write/*counter_collection.csv) "$OUT/pmc_traffic.json"
+python3 scripts/pmc_traffic.py $(ls "$OUT"/pmc_fetch/*counter_collection.csv) $(ls "$OUT"/pmc_write/*counter_collection.csv) "$OUT/pmc_traffic.json" --tiles 8
 python3 scripts/pmc_traffic.py $(ls "$OUT"/pv_fetch/*counter_collection.csv) $(ls "$OUT"/pv_write/*counter_collection.csv) "$OUT/pmc_traffic_pview.json" --pview
 python3 scripts/pmc_summary.py "pview_tick_kernel<8, false" $(ls "$OUT"/pv_sq/*counter_collection.csv) --json "$OUT/pmc_sq_pview.json"
 echo done

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of the fused tick kernel from rocprofv3 PMC passes.
 
-    python scripts/pmc_traffic.py <pmc_fetch.csv> <pmc_write.csv> [out.json] [--pview]
+    python scripts/pmc_traffic.py <pmc_fetch.csv> <pmc_write.csv> [out.json] [--pview] [--tiles T]
 
 --pview: the partial-view tick kernel (8-B/lane view loads and stores) instead of the
-full-view fused tick kernel.
+full-view fused tick kernel.  --tiles T: the full view ran as T column tiles (T launches per
+tick); bytes_per_tick = T x the per-launch average.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts half of
 the bytes of a wide (16 B/lane) coalesced streaming read, which is every load of this
@@ -34,6 +35,11 @@ def main():
         name = "pview_tick_kernel (partial-view union/fold/evict)"
         NOTE = ("FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
                 "loads: uncalibrated for that width, MI355X_MICROARCH.md HBM section)")
+    tiles = 1
+    if "--tiles" in sys.argv:
+        i = sys.argv.index("--tiles")
+        tiles = int(sys.argv[i + 1])
+        del sys.argv[i:i + 2]
     fetch, n1 = per_launch(sys.argv[1], "FETCH_SIZE")
     write, n2 = per_launch(sys.argv[2], "WRITE_SIZE")
     out = {
@@ -44,6 +50,8 @@ def main():
         "read_bytes_per_launch": fetch * 1024 * 2,
         "write_bytes_per_launch": write * 1024,
         "bytes_per_launch": fetch * 1024 * 2 + write * 1024,
+        "launches_per_tick": tiles,
+        "bytes_per_tick": (fetch * 1024 * 2 + write * 1024) * tiles,
         "correction": NOTE,
     }
     s = json.dumps(out, indent=1)
