@@ -211,7 +211,12 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     xch_ms = (p1["csr_ms"] - p0["csr_ms"]) / launches
     bytes_per_launch = ((2.0 * rounds + delivered) * V * 8.0 + csr * 4.0) / steps
     xgmi = (p1["xgmi_bytes"] - p0["xgmi_bytes"]) / steps
-    ev = event_summary(eng, nodes, warmup + steps, dist) if events else None
+    ev = None
+    if events:
+        from gossip_protocol_amd import _lib
+        ev = event_summary(eng, nodes, warmup + steps, dist,
+                           _lib.fail_schedule(nodes, PV_KW["seed"], PV_KW["fail_mode"],
+                                              PV_KW["fail_tick"], PV_KW["fail_ppm"]))
     eng.close()
     if dist is not None:
         t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device=_dev())
@@ -329,7 +334,11 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
     launches = max(perf1["merge_launches"] - perf0["merge_launches"], 1)
     kern_ms = (perf1["merge_ms"] - perf0["merge_ms"]) / launches
     csr_ms = (perf1["csr_ms"] - perf0["csr_ms"]) / launches
-    ev = event_summary(eng, nodes, warmup + steps, dist) if events else None
+    ev = None
+    if events:
+        from gossip_protocol_amd import _lib
+        ev = event_summary(eng, nodes, warmup + steps, dist,
+                           _lib.fail_schedule(nodes, SEED, FAIL_RANDOM, FAIL_TICK, FAIL_PPM))
     eng.close()
     if dist is not None:
         # per-row counts live on rank 0 only (columns) or on the row's owner (rows): the sum is
@@ -353,49 +362,58 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
             "events": ev, "tiles": shards_total if dist is None else 1}
 
 
-def event_summary(eng, nodes, last_tick, dist):
-    """Per-crashed-node detection latency from the drained event stream: for every node x that
-    some node removed, the tick of the first removal of x and of the last one (every live
-    node has removed it), minus the crash tick.  The reference logs the same removals as
-    "Node x removed at time t" lines (MP1Node.cpp:343, Log.cpp:127-130); the grader measures
-    detection from them (grader/Grader.sh).  Ranks combine per-node first / last / count."""
+def event_summary(eng, nodes, last_tick, dist, crash):
+    """Failure detection read from the drained event stream.  crash: every node's crash tick
+    (gsp_fail_schedule; int32 max = never).  For each node that crashed before the last tick,
+    the first and the last removal of it after its crash (the last = every live node that
+    listed it has removed it) minus its crash tick; removals of nodes that never crashed are
+    counted apart (none in the full view without drops; a partial view's churn).  The reference
+    logs the same removals as "Node x removed at time t" (MP1Node.cpp:343, Log.cpp:127-130) and
+    its grader scores detection from them (Grader.sh).  Ranks combine per-node first / last /
+    count."""
     import numpy as np
     import torch
     from gossip_protocol_amd import _lib
     rec, lost = eng.drain_events()
     kind, tk, _, x = _lib.split_events(rec)
     rem = kind == _lib.EVENT_REMOVE
-    xr, tr = x[rem], tk[rem]
+    xr, tr = x[rem].astype(np.int64), tk[rem].astype(np.int64)
+    crash = np.asarray(crash, np.int64)
+    after = tr > crash[xr]                    # removals of x after its crash
+    live_removes = int((crash[xr] >= last_tick).sum())
+    xa, ta = xr[after], tr[after]
     first = np.full(nodes, 1 << 30, np.int64)
     last = np.full(nodes, -1, np.int64)
-    for t in np.unique(tr)[::-1]:         # descending: the earliest tick is written last
-        first[xr[tr == t]] = t
-    for t in np.unique(tr):
-        last[xr[tr == t]] = t
-    count = np.bincount(xr, minlength=nodes).astype(np.int64)
+    for t in np.unique(ta)[::-1]:             # descending: the earliest tick is written last
+        first[xa[ta == t]] = t
+    for t in np.unique(ta):
+        last[xa[ta == t]] = t
+    count = np.bincount(xa, minlength=nodes).astype(np.int64)
     joins = int((kind == _lib.EVENT_JOIN).sum())
+    n_rec, n_rem = len(rec), int(rem.sum())
     if dist is not None:
         f = torch.from_numpy(first).to(_dev())
         l_ = torch.from_numpy(last).to(_dev())
         c = torch.from_numpy(count).to(_dev())
-        tot = torch.tensor([len(rec), lost, joins], dtype=torch.int64, device=_dev())
+        tot = torch.tensor([n_rec, lost, joins, live_removes, n_rem], dtype=torch.int64,
+                           device=_dev())
         dist.all_reduce(f, op=dist.ReduceOp.MIN)
         dist.all_reduce(l_, op=dist.ReduceOp.MAX)
         dist.all_reduce(c)
         dist.all_reduce(tot)
         first, last, count = f.cpu().numpy(), l_.cpu().numpy(), c.cpu().numpy()
-        n_rec, lost, joins = (int(v) for v in tot.tolist())
-    else:
-        n_rec = len(rec)
-    det = count > 0
+        n_rec, lost, joins, live_removes, n_rem = (int(v) for v in tot.tolist())
+    crashed = crash < last_tick
+    det = crashed & (count > 0)
     stat = lambda a: {"min": int(a.min()), "mean": float(a.mean()), "max": int(a.max())} \
         if len(a) else None
-    return {"records": n_rec, "lost": int(lost), "joins": joins, "removes": int(count.sum()),
-            "crash_tick": FAIL_TICK, "last_tick": last_tick,
-            "crashed_nodes_detected": int(det.sum()),
+    return {"records": n_rec, "lost": int(lost), "joins": joins,
+            "removes": n_rem, "last_tick": last_tick,
+            "crashed_nodes": int(crashed.sum()), "crashed_nodes_detected": int(det.sum()),
             "removes_per_detected_node": float(count[det].mean()) if det.any() else 0.0,
-            "first_detection_latency_ticks": stat(first[det] - FAIL_TICK),
-            "full_detection_latency_ticks": stat(last[det] - FAIL_TICK)}
+            "removes_of_live_nodes": live_removes,
+            "first_detection_latency_ticks": stat((first - crash)[det]),
+            "full_detection_latency_ticks": stat((last - crash)[det])}
 
 
 def summarize_full(r, nodes, steps, world):

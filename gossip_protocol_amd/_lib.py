@@ -189,6 +189,8 @@ SIGNATURES = {
     "gsp_pview_drain_events": (ctypes.c_int, [ctypes.c_void_p, P(c_uint64), c_int64, P(c_int64),
                                               P(c_int64)]),
     "gsp_events_write_log": (ctypes.c_int, [P(c_uint64), c_int64, ctypes.c_char_p]),
+    "gsp_fail_schedule": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_uint64, c_int32, c_int32,
+                                         c_int32, P(c_int32)]),
 }
 
 
@@ -220,6 +222,16 @@ def split_events(rec):
     return ((rec >> np.uint64(62)).astype(np.int32), ((rec >> np.uint64(42)) & np.uint64(0xFFFFF)).astype(np.int32),
             ((rec >> np.uint64(21)) & np.uint64(0x1FFFFF)).astype(np.int32),
             (rec & np.uint64(0x1FFFFF)).astype(np.int32))
+
+
+def fail_schedule(n, seed, mode, tick, ppm, policy=None):
+    """gsp_fail_schedule: every node's crash tick (INT32_MAX = never) as an int32 array."""
+    import numpy as np
+    out = np.zeros(n, np.int32)
+    check(lib().gsp_fail_schedule(ctypes.byref(policy) if policy is not None else None, n, seed,
+                                  mode, tick, ppm, out.ctypes.data_as(P(c_int32))),
+          "gsp_fail_schedule")
+    return out
 
 
 def write_event_log(rec, path):

@@ -92,3 +92,15 @@ JoinPlan join_plan(const std::vector<int32_t> &start, int32_t max_tick) {
 }
 
 }  // namespace gsp
+
+extern "C" int gsp_fail_schedule(const gsp_policy *pol, int32_t n, uint64_t seed, int32_t mode,
+                                 int32_t tick, int32_t ppm, int32_t *out) {
+    GSP_REQUIRE(out && n >= 1 && mode >= 0 && mode <= 4, GSP_ERR_INVALID,
+                "gsp_fail_schedule: n=%d mode=%d", n, mode);
+    gsp_policy none{};
+    const gsp_policy &p = pol ? *pol : none;
+    if (int rc = gsp::validate_policy(p, n)) return rc;
+    const std::vector<int32_t> f = gsp::fail_ticks(p, n, seed, mode, tick, ppm);
+    std::copy(f.begin(), f.end(), out);
+    return GSP_OK;
+}

@@ -235,6 +235,13 @@ typedef struct {
     gsp_fail_event fail_events[GSP_MAX_FAIL_EVENTS];
 } gsp_policy;
 
+/* The crash tick of every node under a failure schedule -- the first event (mode, tick, ppm of
+ * gsp_scale_params / gsp_pview_params) and policy's further events, with the engines' own
+ * Philox draws; INT32_MAX = never.  Host only (no device needed): lets a driver know which
+ * nodes crashed, e.g. to measure failure detection from the event stream.  pol may be NULL. */
+int gsp_fail_schedule(const gsp_policy *pol, int32_t n, uint64_t seed, int32_t mode, int32_t tick,
+                      int32_t ppm, int32_t *out);
+
 /* ------------------------------------------------------------------------------------
  * SCALE engine (full view, packed entries, device-resident tick loop)
  * ---------------------------------------------------------------------------------- */

@@ -69,6 +69,14 @@ def _worker(rank, world, port, q):
     gd.make_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world,
                                                           rows=kw.get("layout") == "rows")
     gd.make_pview_rank_engine = lambda n, dev, **kw: FakeEngine(n, rank, world, pview=True)
+    import numpy as np
+    from gossip_protocol_amd import _lib
+
+    def crash_ticks(n, *a, **k):                     # nodes 5 and 7 crash at t = 0
+        c = np.full(n, np.iinfo(np.int32).max, np.int32)
+        c[[5, 7]] = 0
+        return c
+    _lib.fail_schedule = crash_ticks
     import bench
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
@@ -124,8 +132,10 @@ def test_bench_two_ranks_gloo():
     ev = d["events"]                                  # per-node first / last over the ranks
     assert ev["records"] == 6 and ev["joins"] == 1 and ev["removes"] == 5 and ev["lost"] == 0
     assert ev["crashed_nodes_detected"] == 2 and ev["removes_per_detected_node"] == 2.5
-    assert ev["first_detection_latency_ticks"] == {"min": 1, "mean": 10.5, "max": 20}
-    assert ev["full_detection_latency_ticks"] == {"min": 3, "mean": 12.0, "max": 21}
+    assert ev["crashed_nodes"] == 2 and ev["removes_of_live_nodes"] == 0
+    assert ev["first_detection_latency_ticks"] == {"min": 11, "mean": 20.5, "max": 30}
+    assert ev["full_detection_latency_ticks"] == {"min": 13, "mean": 22.0, "max": 31}
     assert ev["kernel_overhead_frac"] == 0.0
     pe = pv["events"]                                 # the partial view's removes-only run
+    assert "error" not in pe, pe
     assert pe["kinds"] == 4 and pe["crashed_nodes_detected"] == 2 and pe["kernel_overhead_frac"] == 0.0

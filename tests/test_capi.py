@@ -166,3 +166,23 @@ def test_scale_params_extended_keys(tmp_path):
         f.write("BOGUS: 1\n")
     assert L.gsp_pview_params_from_conf(path.encode(), ctypes.byref(_lib.GspPviewParams())) == -1
     assert b"unknown key BOGUS" in L.gsp_last_error()
+
+
+def test_fail_schedule_matches_oracle():
+    """gsp_fail_schedule (host only) = the oracle's crash ticks, every mode and multi-event
+    policies (the schedule bench.py uses to score failure detection from the event stream)."""
+    import numpy as np
+    from gossip_protocol_amd import _lib
+    from gossip_protocol_amd.scale import make_policy
+    from tests.oracle_binding import ScaleOracle
+    from tests.oracle_binding import make_policy as oracle_policy
+    ev = [(7, 3, 0), (9, 2, 40000)]
+    for mode, ppm in ((1, 20000), (2, 50000), (3, 0), (4, 0)):
+        for events in ((), ev):
+            got = _lib.fail_schedule(3000, 77, mode, 5, ppm, make_policy(fail_events=list(events)))
+            orc = ScaleOracle(3000, fail_mode=mode, fail_tick=5, fail_ppm=ppm,
+                              seed=77, policy=oracle_policy(fail_events=list(events)))
+            want = np.array([orc.fail_tick(r) for r in range(3000)], np.int32)
+            orc.close()
+            assert np.array_equal(got, want), (mode, events)
+            assert (got < np.iinfo(np.int32).max).any()
