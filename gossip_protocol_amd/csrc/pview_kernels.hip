@@ -213,11 +213,12 @@ __device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r,
 
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
-// kExt: the protocol extensions are compiled in -- TFAIL payload filter, JOINREP (jrep:
+// kExt: the protocol extensions compiled in, a bit mask -- kExtPol: TFAIL payload filter, JOINREP (jrep:
 // message 1 is a JOINREP whose payload is node 0's view cut to the bounded introducer list),
 // SWIM (pcol / pok: the probe of t - 1, target id or kNoId, answered) and the event stream;
 // the plain protocol (config 5) runs the kernel without them.
-template <int kBlocks, bool kExt>
+constexpr int kExtEv = 1, kExtPol = 2;   // kExt bits: event stream; TFAIL / SWIM / JOINREP
+template <int kBlocks, int kExt>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
                                              int32_t k, uint64_t ent0, int32_t my_slot,
                                              const uint32_t (&ssrc)[kPvMaxInbox], bool jrep,
@@ -251,10 +252,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             const uint64_t *row = (m == 1 && jrep) ? a.intro
                                   : sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
             ent[m] = __builtin_nontemporal_load(row + tid);
-            if (kExt && !gossiped(ent[m])) ent[m] = kPvEmpty;
+            if ((kExt & kExtPol) && !gossiped(ent[m])) ent[m] = kPvEmpty;
         }
     }
-    if constexpr (kBlocks > 1 && kExt) if (jrep) {   // block-uniform: node 0's gossiped members
+    if constexpr (kBlocks > 1 && (kExt & kExtPol)) if (jrep) {   // block-uniform: node 0's gossiped members
         const bool g = ent[1] != kPvEmpty;
         uint32_t cnt0 = 0;
         const uint32_t rank = block_scan(g ? 1u : 0u, &cnt0, sh.keys[1]);   // keys[1] is free here
@@ -272,7 +273,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
         kpos[m] = tid;
-        if (kExt && m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
+        if ((kExt & kExtPol) && m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
             const bool ok = ent[m] != kPvEmpty;
             uint32_t cnt = 0;
             const uint32_t pos = block_scan(ok ? 1u : 0u, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
@@ -285,8 +286,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     for (int m = 0; m < kBlocks; ++m) {
         const bool ok = ent[m] != kPvEmpty;
         merged += (m >= 1 && ok) ? 1u : 0u;
-        if (kExt && ((kpad >> m) & 1u)) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted tail
-        if (!kExt || kpos[m] >= 0)
+        if ((kExt & kExtPol) && ((kpad >> m) & 1u)) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted tail
+        if (!(kExt & kExtPol) || kpos[m] >= 0)
             sh.keys[0][m * kSlots + kpos[m]] =
                 ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
         sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
@@ -442,12 +443,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         if (!aown) continue;
         if (ajs && !adone) av = pv_event(av, t5);
         if (x == uint32_t(r) || !av) continue;                  // never list yourself
-        if (kExt && x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
-        if (!ae0) { joins++; hsum += pv_hash(S_join, x); if (kExt) jmask |= 1u << e; }
+        if ((kExt & kExtPol) && x == pcol) av = (av & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));   // SWIM answer
+        if (!ae0) { joins++; hsum += pv_hash(S_join, x); if (kExt & kExtEv) jmask |= 1u << e; }
         if (((t5 - av) & 31u) >= tr) {                          // TREMOVE scan
             removes++;
             hsum += pv_hash(S_remove, x);
-            if (kExt) rmask |= 1u << e;
+            if (kExt & kExtEv) rmask |= 1u << e;
             continue;
         }
         res[e] = av;
@@ -473,7 +474,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
     }
 
-    if (kExt && a.ev.buf) {                              // event stream: joins and removes
+    if ((kExt & kExtEv) && a.ev.buf) {                   // event stream: joins and removes
         if (!(a.ev.kinds & GSP_EVENTS_JOIN)) jmask = 0;
         if (!(a.ev.kinds & GSP_EVENTS_REMOVE)) rmask = 0;
         const uint32_t amask = (a.ev.kinds & GSP_EVENTS_JOIN) ? adopt : 0u;
@@ -642,7 +643,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         uint32_t *Wid = sh.keys[cur];
         uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
-        const bool ev_on = kExt && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
+        const bool ev_on = (kExt & kExtEv) && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
         if (ev_on) {
             const int32_t tk = int32_t(need2) - int32_t(tie_before);
             const uint32_t kept = nk + uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
@@ -734,7 +735,7 @@ __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) 
 
 // One non-init row: the own view slot and the receipt record are requested first (their
 // latencies overlap), then merge, ops, eviction, view write and digest record.
-template <bool kExt>
+template <int kExt>
 __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int32_t lr) {
     const int32_t tid = threadIdx.x, lane = tid & 63;
     const int32_t r = a.row0 + lr;
@@ -754,7 +755,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     const int32_t info = __builtin_amdgcn_readfirstlane(info_v);
     const int32_t k = info & 7, k_all = info >> 3;
     // a JOINREP (sender kJoinRepSrc) sorts first; its sender event is node 0's
-    const bool jrep = kExt && k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
+    const bool jrep = (kExt & kExtPol) && k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
     uint32_t ssrc[kPvMaxInbox];
 #pragma unroll
     for (int jj = 0; jj < kPvMaxInbox; ++jj)
@@ -764,7 +765,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     // the swim paths survived its drop draw (paths sent at t - 1)
     uint32_t pcol = kNoId;
     bool pok = false;
-    if (kExt && a.swim > 0) {
+    if ((kExt & kExtPol) && a.swim > 0) {
         const int32_t p = __builtin_amdgcn_readfirstlane(a.ping[lr]);
         if (p >= 0) {
             pcol = uint32_t(p);
@@ -840,7 +841,7 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
 // workgroup: a software-pipelined variant (the next row's record, own view and first sender
 // views requested while the current row merged, two rows per workgroup) measured 4-8 % slower
 // -- other resident rows already hide the HBM round trips.
-template <int kWaves, bool kExt>
+template <int kWaves, int kExt>
 __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared sh;
     pv_row<kExt>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
@@ -1066,14 +1067,20 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     if (!pv_args_ok(a)) return hipErrorInvalidValue;
     if (a.rows == 0) return hipSuccess;
     const dim3 g(unsigned(a.rows)), blk(kPvBlock);
-    // the protocol extensions in use (TFAIL, SWIM, joins, events) select the kExt kernel
-    const bool ext = a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr || a.ev.buf != nullptr;
-    if (ext) {
-        if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8, true>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((pview_tick_kernel<7, true>), g, blk, 0, st, a);
-    } else {
-        if (a.waves == 8) hipLaunchKernelGGL((pview_tick_kernel<8, false>), g, blk, 0, st, a);
-        else hipLaunchKernelGGL((pview_tick_kernel<7, false>), g, blk, 0, st, a);
+    // the protocol extensions in use select the kernel: kExtPol for TFAIL / SWIM / joins,
+    // kExtEv for the event stream (the plain protocol runs neither)
+    const int ext = ((a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr) ? kExtPol : 0) |
+                    (a.ev.buf != nullptr ? kExtEv : 0);
+    const bool w8 = a.waves == 8;
+    switch (ext) {
+        case 0: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, 0>), g, blk, 0, st, a);
+                else hipLaunchKernelGGL((pview_tick_kernel<7, 0>), g, blk, 0, st, a); break;
+        case kExtEv: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtEv>), g, blk, 0, st, a);
+                     else hipLaunchKernelGGL((pview_tick_kernel<7, kExtEv>), g, blk, 0, st, a); break;
+        case kExtPol: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtPol>), g, blk, 0, st, a);
+                      else hipLaunchKernelGGL((pview_tick_kernel<7, kExtPol>), g, blk, 0, st, a); break;
+        default: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtPol | kExtEv>), g, blk, 0, st, a);
+                 else hipLaunchKernelGGL((pview_tick_kernel<7, kExtPol | kExtEv>), g, blk, 0, st, a); break;
     }
     launch_send_and_digest(a, st);
     return hipGetLastError();

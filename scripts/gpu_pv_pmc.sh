@@ -19,5 +19,5 @@ pass sq2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU S
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
 cd "$GRAFT_REPO_ROOT"
-python3 scripts/pmc_summary.py "pview_tick_kernel<8, false" $(ls "$OUT"/*/run_counter_collection.csv) --json "$OUT/summary.json"
+python3 scripts/pmc_summary.py "pview_tick_kernel<8, 0>" $(ls "$OUT"/*/run_counter_collection.csv) --json "$OUT/summary.json"
 echo done

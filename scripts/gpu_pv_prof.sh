@@ -20,5 +20,5 @@ pass() {
 pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS
 pass sq2 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA SQ_INSTS_VALU
 cd "$GRAFT_REPO_ROOT"
-python3 scripts/pmc_summary.py "pview_tick_kernel<8, false" $(ls "$OUT"/*/run_counter_collection.csv) --json "$OUT/summary.json"
+python3 scripts/pmc_summary.py "pview_tick_kernel<8, 0>" $(ls "$OUT"/*/run_counter_collection.csv) --json "$OUT/summary.json"
 echo done

@@ -31,7 +31,7 @@ def main():
     name = "scale_tick_kernel (fused merge/ops/send)"
     if "--pview" in sys.argv:
         sys.argv.remove("--pview")
-        KERNEL = "pview_tick_kernel<8, false"
+        KERNEL = "pview_tick_kernel<8, 0>"
         name = "pview_tick_kernel (partial-view union/fold/evict)"
         NOTE = ("FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
                 "loads: uncalibrated for that width, MI355X_MICROARCH.md HBM section)")
