@@ -88,8 +88,13 @@ def reference_cpu_baseline(budget_s=8.0):
     if not os.path.exists(REF_APP):
         return None
     src = os.path.join(ROOT, "tests", "golden", "ref", "testcases")
-    rounds = runs = 0
+    rounds = runs = merges = 0
     wall = 0.0
+    try:                    # merges of each run from the pinned restatement (same seed, glibc)
+        from tests.oracle_binding import load_oracle, run_oracle_mp1
+        load_oracle()
+    except Exception:       # noqa: BLE001 -- the oracle library is optional here
+        run_oracle_mp1 = None
     with tempfile.TemporaryDirectory() as tmp:
         os.makedirs(os.path.join(tmp, "testcases"))
         for c in REF_CONFS:
@@ -105,9 +110,13 @@ def reference_cpu_baseline(budget_s=8.0):
                 wall += time.perf_counter() - a
                 with open(os.path.join(tmp, "dbg.log"), "rb") as f:
                     rounds += ref_node_rounds(f.read())
+                if run_oracle_mp1 is not None:
+                    run_oracle_mp1(c, seed, "glibc", os.path.join(tmp, "oracle"))
+                    merges += load_oracle().gsp_oracle_mp1_merges()
                 runs += 1
             seed += 1
     out = {"value": rounds / wall, "unit": "node-rounds/s", "cores": 1, "kind": "reference",
+           "merges_per_s": merges / wall if merges else None,
            "sample": "oracle/_ref/Application (the reference, -O0 as its Makefile builds it), "
                      "%d runs of its 3 testcases (N = 10, 700 ticks, seeds 1..%d), %d node-rounds "
                      "in %.2f s of whole-process wall time, 1 thread" % (runs, seed - 1, rounds, wall)}

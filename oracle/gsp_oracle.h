@@ -128,6 +128,7 @@ int32_t gsp_scale_oracle_remove_scan(int32_t n, int32_t t, int32_t T, int32_t tf
 void gsp_oracle_mp1_set_queue_trace(const char *path);
 /* opt-in bounded introducer list of the exact engine (gsp_params.intro_list); 0 = reference */
 void gsp_oracle_mp1_set_intro_list(int b);
+int64_t gsp_oracle_mp1_merges(void);
 
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x);
 uint64_t gsp_pv_event_mix(int kind, int64_t t, int64_t r, int64_t x);   /* partial view */

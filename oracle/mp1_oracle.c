@@ -130,6 +130,10 @@ int64_t gsp_oracle_mp1_buffer_full_rejects(void) { return g_buffer_full_rejects;
 /* opt-in bounded introducer list (gsp_params.intro_list; 0 = the reference) */
 static int g_intro_list;
 void gsp_oracle_mp1_set_intro_list(int b) { g_intro_list = b; }
+/* member-entry merges of the last run: 1 + |payload| per GOSSIP handled (the exact engine's
+ * gsp_exact_stats.merges) */
+static int64_t g_merges;
+int64_t gsp_oracle_mp1_merges(void) { return g_merges; }
 
 /* ---------------- EmulNet (EmulNet.cpp) ---------------- */
 static void en_send(sim_t *s, int src_node, int dst_id, int type, const entry_t *pl, int npl) {
@@ -226,6 +230,7 @@ static void handle(sim_t *s, int node, msg_t *m) {       /* recvCallBack, MP1Nod
             }
         }
     } else if (m->type == M_GOSSIP) {
+        g_merges += 1 + m->npayload;
         entry_t *e = find(nd, m->src);
         if (e) { e->hb += 1; e->ts = s->t; }
         else add_from_header(s, node, m->src);
@@ -357,6 +362,7 @@ int gsp_oracle_mp1_run(const char *conf_path, uint64_t seed, int rng_mode, int t
     sim_t s;
     memset(&s, 0, sizeof s);
     g_buffer_full_rejects = 0;
+    g_merges = 0;
     g_trace = g_trace_path[0] ? fopen(g_trace_path, "w") : NULL;
     if (read_conf(&s, conf_path) != 0) return -1;
     if (s.n <= 0 || s.n > 1000 || ticks <= 0 || ticks > MAX_TICKS) return -2;

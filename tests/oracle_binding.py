@@ -99,6 +99,7 @@ def load_oracle():
         L.gsp_oracle_mp1_run.restype = ctypes.c_int
         L.gsp_oracle_mp1_buffer_full_rejects.restype = ctypes.c_int64
         L.gsp_oracle_mp1_set_intro_list.argtypes = [ctypes.c_int]
+        L.gsp_oracle_mp1_merges.restype = ctypes.c_int64
         L.gsp_glibc_stream.argtypes = [ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32),
                                        ctypes.c_int64]
         L.gsp_scale_oracle_create.argtypes = [ctypes.POINTER(ScaleCfg)]

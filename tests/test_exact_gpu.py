@@ -66,3 +66,13 @@ def test_exact_bitexact_vs_reference_big(tmp_path, conf, seed, mode):
             pytest.fail("%s differs at line %d:\n got: %s\nwant: %s" % (
                 name, first, gl[first][:300] if first < len(gl) else "<eof>",
                 wl[first][:300] if first < len(wl) else "<eof>"))
+
+
+@pytest.mark.parametrize("conf", CONFS)
+def test_exact_merge_count_matches_oracle(tmp_path, conf):
+    """gsp_exact_stats.merges (1 + |payload| per GOSSIP handled, counted on the device) equals
+    the restatement's count -- the figure bench.py's reference CPU baseline reports per second."""
+    from tests.oracle_binding import load_oracle, run_oracle_mp1
+    got = exact.run_application(conf_path(conf), 1, "glibc", str(tmp_path / "gpu"))["stats"].merges
+    run_oracle_mp1(conf, 1, "glibc", str(tmp_path / "cpu"))
+    assert got == load_oracle().gsp_oracle_mp1_merges() > 0
