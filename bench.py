@@ -311,6 +311,11 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
         kw.update(events=True, event_cap=EVENT_CAP)
     if dist is not None:
         from gossip_protocol_amd.dist import make_rank_engine
+        if tiles is None:     # 8192-column tiles per rank when the slices are wider (N = 2, 4)
+            tiles = TILES // world if (layout == "columns" and world < TILES and TILES % world == 0
+                                       and nodes % (2048 * TILES) == 0) else 1
+        if tiles > 1:
+            kw["tiles"] = tiles
         eng = make_rank_engine(nodes, local, **kw)
     else:
         if tiles is None:
@@ -368,7 +373,7 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
     bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
     return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
             "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout,
-            "events": ev, "tiles": shards_total if dist is None else 1}
+            "events": ev, "tiles": shards_total // (world if dist is not None else 1)}
 
 
 def event_summary(eng, nodes, last_tick, dist, crash):
@@ -446,7 +451,8 @@ def summarize_full(r, nodes, steps, world):
         "config": {"workload": "%s: %d nodes full view, fanout %d, 1%% random crash at t=%d, "
                                "no drops" % (cfg, nodes, FANOUT, FAIL_TICK),
                    "nodes": nodes, "view": nodes, "fanout": FANOUT, "entry_bytes": 2,
-                   "parallelism": "%s%d" % (r["layout"], world) if world > 1 else
+                   "parallelism": ("%s%d" % (r["layout"], world) +
+                                   ("" if r["tiles"] == 1 else "-%dtiles" % r["tiles"])) if world > 1 else
                    "1gpu" if r["tiles"] == 1 else "1gpu-%dtiles" % r["tiles"]},
         "merges_per_s": r["merges"] / r["el"],
         "xgmi_bytes_per_tick": r["xgmi_tick"],

@@ -162,6 +162,9 @@ SIGNATURES = {
                                              ctypes.c_void_p, P(ctypes.c_void_p)]),
     "gsp_scale_create_group": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
                                               P(ctypes.c_void_p)]),
+    "gsp_scale_create_rank_tiled": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
+                                                   c_int32, c_int32, ctypes.c_void_p,
+                                                   P(ctypes.c_void_p)]),
     "gsp_scale_create_rank_layout": (ctypes.c_int, [P(GspScaleParams), ctypes.c_int, c_int32,
                                                     c_int32, ctypes.c_void_p, c_int32,
                                                     P(ctypes.c_void_p)]),

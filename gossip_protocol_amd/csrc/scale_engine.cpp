@@ -149,7 +149,7 @@ struct gsp_scale {
         a.out_dst = sh.out_dst.p;
         a.deg = sh.deg.p;
         a.ping = (shared ? s0 : sh).ping.p;
-        a.bitmap = shared ? s0.bitmap.p + size_t(sh.g) * size_t(p.n) * size_t(stride / 8) : sh.bitmap.p;
+        a.bitmap = shared ? s0.bitmap.p + size_t(sh.g - rank) * size_t(p.n) * size_t(stride / 8) : sh.bitmap.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
         a.err = sh.err.p;
         a.max_segment = max_segment;
@@ -174,7 +174,9 @@ struct gsp_scale {
         r.cnt_total = sh.cnt_total[t & 1].p;
         r.bitmap = sh.bitmap.p;
         r.picks = sh.picks.p;
-        r.tiled = shared ? 1 : 0;       // one launch resolves every shard's ranks
+        r.tiled = shared ? 1 : 0;       // one launch resolves the ranks of every local shard
+        r.tile_lo = rank;
+        r.tile_cnt = int32_t(local.size());
         r.tile_bytes = int64_t(p.n) * (stride / 8);
         r.swim = p.swim;
         r.ping = sh.ping.p;
@@ -245,8 +247,8 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
         GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
         GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards * (s->shared ? 2 : 1)));
         GSP_HIP(sh.picks.alloc(size_t(n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0))));
-        // shared: every shard's bitmap, one region per shard (the resolve reads them all)
-        GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8) * (s->shared ? size_t(s->shards) : 1)));
+        // shared: every local shard's bitmap, one region each (the resolve reads them all)
+        GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8) * (s->shared ? s->local.size() : 1)));
     }
     if (s->rowmode)
         GSP_HIP(sh.x.alloc(s->shards, s->pair_cap, s->msg_cap, int32_t(s->stride / 4),
@@ -277,9 +279,16 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
 }
 
 // all-gather of every shard's per-row slice counts into every shard's cnt_all[G][n]
-int exchange_counts(gsp_scale *s) {
+int exchange_counts(gsp_scale *s, int32_t t) {
     const size_t n = size_t(s->p.n);
-    if (s->shared) return GSP_OK;         // the shards wrote shard 0's cnt_all directly
+    if (s->shared) {                      // the local shards wrote shard 0's cnt_all directly
+        if (!s->comm) return GSP_OK;
+        // in place: this rank's block of local-shard rows -> every rank's cnt_all[t & 1]
+        const size_t L = s->local.size();
+        int32_t *all = s->local[0].cnt_all.p + size_t(t & 1) * size_t(s->shards) * n;
+        GSP_NCCL(ncclAllGather(all + size_t(s->rank) * n, all, L * n, ncclInt32, s->comm, s->st));
+        return GSP_OK;
+    }
     if (s->comm) {
         Shard &sh = s->local[0];
         GSP_NCCL(ncclAllGather(sh.cnt_slice.p, sh.cnt_all.p, n, ncclInt32, s->comm, s->st));
@@ -311,17 +320,25 @@ int exchange_picks(gsp_scale *s) {
 
 // message generation for tick t (columns: after the slices are merged)
 int resolve_sends(gsp_scale *s, int32_t t) {
-    if (s->shared) {                     // one resolve over every shard's ranks, one finalize
+    const double G = double(s->shards), n = double(s->p.n);
+    if (s->shared) {                     // one resolve over every local shard's ranks, one finalize
+        if (s->comm) {                   // ... between the ranks' count and pick collectives
+            const double W = G / double(s->local.size());
+            s->perf.xgmi_bytes += (W - 1.0) * (n * 4.0 * double(s->local.size()) +
+                                               2.0 * n * (s->p.fanout + (s->p.swim > 0 ? 1 : 0)) * 4.0 / W);
+            if (int rc = exchange_counts(s, t)) return rc;
+        }
         GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(s->local[0], t), s->st));
+        if (s->comm)
+            if (int rc = exchange_picks(s)) return rc;
         GSP_HIP(gsp::launch_scale_finalize(s->resolve_args(s->local[0], t), s->st));
         return GSP_OK;
     }
     // egress per shard of ring collectives: all-gather (G-1)/G of G*n*4 B, all-reduce
     // 2 (G-1)/G of n*f*4 B
-    const double G = double(s->shards), n = double(s->p.n);
     s->perf.xgmi_bytes += double(s->local.size()) * (G - 1.0) *
                           (n * 4.0 + 2.0 * n * (s->p.fanout + (s->p.swim > 0 ? 1 : 0)) * 4.0 / G);
-    if (int rc = exchange_counts(s)) return rc;
+    if (int rc = exchange_counts(s, t)) return rc;
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_resolve(s->resolve_args(sh, t), s->st));
     if (int rc = exchange_picks(s)) return rc;
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_finalize(s->resolve_args(sh, t), s->st));
@@ -482,7 +499,14 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     // a communicator always runs the sharded protocol (with one rank it exercises RCCL alone)
     const bool sharded = shards > 1 || nccl_id != nullptr;
     s->sliced = sharded && layout == GSP_SHARD_COLUMNS;
-    s->shared = s->sliced && nccl_id == nullptr && local_shards > 1 && local_shards == shards;
+    // shared: every shard of this engine shares shard 0's CSR / counts / picks / sends -- an
+    // in-process group (all shards here), or the column tiles of one rank (a communicator over
+    // shards / local_shards ranks, each holding local_shards consecutive shards)
+    s->shared = s->sliced && local_shards > 1 && (nccl_id != nullptr || local_shards == shards);
+    GSP_REQUIRE(nccl_id == nullptr || local_shards == 1 ||
+                    (layout == GSP_SHARD_COLUMNS && shards % local_shards == 0 && rank % local_shards == 0),
+                GSP_ERR_INVALID, "gsp_scale: %d local tiles of %d column shards at shard %d", local_shards,
+                shards, rank);
     if (const char *sx = std::getenv("GSP_SCALE_SHARED")) s->shared = s->shared && std::atoi(sx) != 0;
     s->rowmode = sharded && layout == GSP_SHARD_ROWS;
     const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
@@ -525,7 +549,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     if (nccl_id) {
         ncclUniqueId id;
         std::memcpy(&id, nccl_id, sizeof id);
-        GSP_NCCL(ncclCommInitRank(&s->comm, shards, id, rank));
+        GSP_NCCL(ncclCommInitRank(&s->comm, shards / local_shards, id, rank / local_shards));
     }
     s->local.resize(size_t(local_shards));
     for (int32_t i = 0; i < local_shards; ++i) {
@@ -568,6 +592,14 @@ int gsp_scale_create_rank_layout(const gsp_scale_params *p, int device, int32_t 
                                  int32_t world, const void *nccl_id, int32_t layout, gsp_scale **out) {
     GSP_REQUIRE(nccl_id || world == 1, GSP_ERR_INVALID, "gsp_scale_create_rank_layout: NULL nccl id");
     return scale_build(p, device, world, rank, 1, nccl_id, layout, out);
+}
+
+int gsp_scale_create_rank_tiled(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
+                                int32_t tiles, const void *nccl_id, gsp_scale **out) {
+    GSP_REQUIRE(nccl_id, GSP_ERR_INVALID, "gsp_scale_create_rank_tiled: NULL nccl id");
+    GSP_REQUIRE(tiles >= 1 && world >= 1 && int64_t(world) * tiles <= 64, GSP_ERR_INVALID,
+                "gsp_scale_create_rank_tiled: world=%d tiles=%d", world, tiles);
+    return scale_build(p, device, world * tiles, rank * tiles, tiles, nccl_id, GSP_SHARD_COLUMNS, out);
 }
 
 int gsp_scale_nccl_id(void *out, size_t cap) {

@@ -683,9 +683,10 @@ __global__ void __launch_bounds__(256) scale_resolve_kernel(ScaleResolveArgs a) 
     auto resolve = [&](uint32_t rk) -> int32_t {        // wave-uniform rank -> column or -1
         const unsigned long long own = __ballot(lane < a.shards && rk >= cpre && rk < cpre + c);
         const int32_t g = __builtin_ffsll(own) - 1;
-        if (g != a.shard && !a.tiled) return -1;        // another shard resolves it
+        if (a.tiled ? (g < a.tile_lo || g >= a.tile_lo + a.tile_cnt) : g != a.shard)
+            return -1;                                   // another shard / rank resolves it
         if (g != bm_g) {
-            bm = reinterpret_cast<const uint32_t *>(a.bitmap + (a.tiled ? int64_t(g) * a.tile_bytes : 0) +
+            bm = reinterpret_cast<const uint32_t *>(a.bitmap + (a.tiled ? int64_t(g - a.tile_lo) * a.tile_bytes : 0) +
                                                     int64_t(s) * (a.stride >> 3));
             lane_cnt = 0;
             for (int32_t w = 0; w < per; ++w) lane_cnt += __builtin_popcount(bm[lane * per + w]);

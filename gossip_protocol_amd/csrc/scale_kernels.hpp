@@ -126,8 +126,10 @@ struct ScaleResolveArgs {
     int32_t swim;                // SWIM probing: picks hold fanout + 1 slots per sender, the
                                  // last one the probe target; finalize copies it to ping[]
     int64_t stride;              // slice width
-    int32_t tiled;               // 1: every shard's bitmap is at bitmap + g * tile_bytes and this
-                                 // launch resolves the ranks of every shard (in-process group)
+    int32_t tiled;               // 1: local shards tile_lo .. tile_lo + tile_cnt - 1 keep their
+                                 // bitmaps at bitmap + (g - tile_lo) * tile_bytes and this launch
+                                 // resolves the ranks of all of them (shared shards)
+    int32_t tile_lo, tile_cnt;
     int64_t tile_bytes;
     uint64_t seed;
     const int32_t *fail_tick;

@@ -41,6 +41,8 @@ class ScaleEngine:
 
     group=G (> 1): G shards inside this process on `device` (exchange by device copies).
     rank/world/nccl_id: this process holds shard `rank` of `world` (exchange over RCCL).
+    tiles (with nccl_id): this rank runs its columns as `tiles` column tiles (shared exchange
+    inside the rank, gsp_scale_create_rank_tiled); group: G in-process column tiles of one GPU.
     layout: "columns" (column slices of every row) or "rows" (row blocks; sender rows move
     between shards).  Default: one GPU, full rows, fused tick kernel.
     tfail > 0: TFAIL suspicion (members tfail or more ticks stale are listed but not gossiped,
@@ -52,7 +54,7 @@ class ScaleEngine:
     def __init__(self, n, fanout=3, drop_pct=0, tremove=20, h0=1, fail_mode=FAIL_NONE,
                  fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0, group=1,
                  rank=0, world=1, nccl_id=None, layout="columns", tfail=0, swim=0, policy=None,
-                 events=False, event_cap=0, params=None):
+                 events=False, event_cap=0, params=None, tiles=1):
         if params is None:
             params = _lib.GspScaleParams(n=n, fanout=fanout, drop_pct=drop_pct, tremove=tremove,
                                          h0=h0, fail_mode=fail_mode, fail_tick=fail_tick,
@@ -63,7 +65,12 @@ class ScaleEngine:
         n, fanout = params.n, params.fanout
         self._h = ctypes.c_void_p()
         lay = LAYOUTS[layout]
-        if nccl_id is not None:
+        if nccl_id is not None and tiles > 1:        # column tiles of this rank (columns)
+            idbuf = ctypes.create_string_buffer(nccl_id, 128)
+            check(lib().gsp_scale_create_rank_tiled(ctypes.byref(self.params), device, rank, world,
+                                                    tiles, idbuf, ctypes.byref(self._h)),
+                  "gsp_scale_create_rank_tiled")
+        elif nccl_id is not None:
             idbuf = ctypes.create_string_buffer(nccl_id, 128)
             check(lib().gsp_scale_create_rank_layout(ctypes.byref(self.params), device, rank, world,
                                                      idbuf, lay, ctypes.byref(self._h)),

@@ -329,6 +329,13 @@ int gsp_scale_create_rank(const gsp_scale_params *p, int device, int32_t rank, i
                           const void *nccl_id, gsp_scale **out);
 int gsp_scale_create_group(const gsp_scale_params *p, int device, int32_t shards,
                            gsp_scale **out);
+/* One process per GPU with `tiles` column tiles per rank: the job has world * tiles column
+ * shards, rank r holds shards [r * tiles, (r + 1) * tiles) and runs them as one GPU's tiles
+ * (shared CSR / counts / picks, DESIGN.md "Column tiles"); the ranks exchange the counts of
+ * their tiles (all-gather) and the picks (all-reduce MAX) over RCCL.  Results are identical to
+ * gsp_scale_create. */
+int gsp_scale_create_rank_tiled(const gsp_scale_params *p, int device, int32_t rank, int32_t world,
+                                int32_t tiles, const void *nccl_id, gsp_scale **out);
 /* Sharding layout of a multi-shard job.
  *   GSP_SHARD_COLUMNS  shard g owns a column slice of every row (above; O(n) exchange)
  *   GSP_SHARD_ROWS     shard g owns rows [floor(g n / G), floor((g + 1) n / G)); each tick the

@@ -324,3 +324,45 @@ def test_capacity_error_stops_the_job(monkeypatch):
     with ScaleEngine(256, fanout=8, max_ticks=10) as eng:   # the default bound: no error
         eng.step(3)
         assert eng.digest(3)["node_rounds"] == 256
+
+
+@pytest.mark.parametrize("tiles", [2, 4])
+@pytest.mark.parametrize("variant", ["plain", "tfail_swim", "policy_events"])
+def test_rccl_rank_path_tiled(tiles, variant):
+    """A rank holding `tiles` column tiles (gsp_scale_create_rank_tiled) over an RCCL
+    communicator of one rank: the tiles share the rank's CSR / counts / picks, the counts of its
+    tiles go through the in-place all-gather and the picks through the all-reduce MAX.  Every
+    digest, the message list and sampled rows equal the oracle."""
+    from gossip_protocol_amd.scale import make_policy, nccl_unique_id
+    from tests.oracle_binding import make_policy as oracle_policy
+    n, ticks = 4096 * tiles, 14
+    kw = dict(fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=5, fail_ppm=20000, seed=6)
+    pol = None
+    if variant == "tfail_swim":
+        kw.update(tfail=5, swim=2)
+    if variant == "policy_events":
+        # 20 joiners a tick (step_rate 0.05): every new node gossips to the introducer first, so
+        # a burst of > 1024 joiners in one tick would overflow node 0's segment (capacity error)
+        pol = dict(drop_window=(2, 9), step_rate=0.05, intro_list=4, fail_events=[(8, 3, 0)])
+    orc = ScaleOracle(n, policy=oracle_policy(**pol) if pol else None, **kw)
+    with ScaleEngine(n, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id(), tiles=tiles,
+                     policy=make_policy(**pol) if pol else None,
+                     events=variant == "policy_events", **kw) as eng:
+        assert eng.layout()[0] == tiles
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, t
+            if variant == "policy_events":
+                from gossip_protocol_amd import _lib
+                rec, lost = eng.drain_events()
+                k, tk, r, x = _lib.split_events(rec)
+                ok, orr, ox = orc.events()
+                assert lost == 0 and sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                    sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), t
+        src, dst = orc.messages()
+        m = eng.messages()
+        assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+            sorted(zip(src.tolist(), dst.tolist()))
+        _compare_state(eng, orc, n, range(0, n, 131))
+    orc.close()
