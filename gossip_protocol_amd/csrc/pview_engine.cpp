@@ -73,6 +73,7 @@ struct gsp_pview {
     int32_t tick = 0;
     bool timing = true;
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
+    bool split = true;           // k <= 3 rows as 128-lane rows (GSP_PV_SPLIT=0 turns it off)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
@@ -137,6 +138,7 @@ struct gsp_pview {
         a.order = sort_rows ? sh.order.p : nullptr;
         a.prof = sh.prof.p;
         a.waves = waves;
+        a.split = split ? 1 : 0;
         a.ev = sh.ev.args();
         return a;
     }
@@ -365,6 +367,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
+    if (const char *sp = std::getenv("GSP_PV_SPLIT")) s->split = std::atoi(sp) != 0;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);

@@ -84,9 +84,10 @@ __device__ inline uint32_t key_id(uint32_t k) { return k >> 11; }
 __device__ inline uint32_t key_src(uint32_t k) { return (k >> 8) & 7u; }
 __device__ inline uint32_t key_slot(uint32_t k) { return k & 255u; }
 
-// exclusive block scan over the 256 lanes; *total = sum of all lanes.  One barrier: the
-// caller alternates between two s_wave buffers, so a buffer is rewritten only after a later
-// scan's barrier has retired every read of it.
+// exclusive block scan over the NT lanes of a row; *total = sum of all lanes.  One barrier:
+// the caller alternates between two s_wave buffers, so a buffer is rewritten only after a
+// later scan's barrier has retired every read of it.
+template <int NT = kPvBlock>
 __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_wave) {
     const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t incl = wave_incl_scan(v);
@@ -94,7 +95,7 @@ __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_w
     __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NT / 64; ++q) {
         const uint32_t x = s_wave[q];
         before += q < wave ? x : 0u;
         all += x;
@@ -140,22 +141,29 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
     }
 }
 
-// LDS of one row (20 KB: 8 rows per CU).  keys[cur] (the sorted union C) is dead once the
-// fold is done and then holds: the kept ids W [0, 256), the kept values (u16) at word 512,
-// the exact hb histogram of an e >= 31 boundary bin (2048 u16 bins) at words [1024, 2048).
-// keys[cur ^ 1] (the last merge level's source) is dead after the tree and holds the (age,
-// hb) eviction bins (1024 u16 counters, words [512, 1024)), the block-scan buffers (words
-// [2040, 2048)) and, when no eviction is needed, the survivor ids U (words [0, 256)).
+// LDS of one row: kKeys = 2048 (up to 8 sources, 20 KB: 8 rows per CU) or 1024 (up to 4
+// sources, 10 KB: 16 rows of 128 lanes per CU).  keys[cur] (the sorted union C) is dead once
+// the fold is done and then holds: the kept ids W [0, 256), the kept values (u16) at word
+// 512, and before them the exact hb histogram of an e >= 31 boundary bin (2048 u16 bins,
+// 1024 words at kHist; consumed before the scan that precedes the W writes).  keys[cur ^ 1]
+// (the last merge level's source) is dead after the tree and holds the (age, hb) eviction
+// bins (1024 u16 counters, words [512, 1024)), the block-scan buffers (8 words at kScan) and,
+// when no eviction is needed, the survivor ids U (words [0, 256)).
+template <int kKeys>
 struct alignas(16) PvShared {
-    uint32_t keys[2][kMaxKeys];          // merge ping-pong; then the regions above
-    uint16_t vals[kMaxKeys];             // values by (source, slot); then survivor values
+    static_assert(kKeys == 1024 || kKeys == 2048, "one or two 1024-key halves");
+    static constexpr int kHist = kKeys - 1024, kScan = kKeys == 2048 ? 2040 : 504;
+    uint32_t keys[2][kKeys];             // merge ping-pong; then the regions above
+    uint16_t vals[kKeys];                // values by (source, slot); then survivor values
 };
-constexpr int kWValWord = 512, kHistWord = 1024, kBinWord = 512;
+constexpr int kWValWord = 512, kBinWord = 512;
 
-__device__ inline int32_t lds_word(const PvShared &sh, const uint32_t *p) {
+template <class Sh>
+__device__ inline int32_t lds_word(const Sh &sh, const uint32_t *p) {
     return int32_t(p - &sh.keys[0][0]);
 }
-__device__ inline int32_t lds_half(const PvShared &sh, const void *p) {
+template <class Sh>
+__device__ inline int32_t lds_half(const Sh &sh, const void *p) {
     return int32_t(reinterpret_cast<const uint16_t *>(p) - reinterpret_cast<const uint16_t *>(&sh));
 }
 
@@ -218,14 +226,17 @@ __device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r,
 // SWIM (pcol / pok: the probe of t - 1, target id or kNoId, answered) and the event stream;
 // the plain protocol (config 5) runs the kernel without them.
 constexpr int kExtEv = 1, kExtPol = 2;   // kExt bits: event stream; TFAIL / SWIM / JOINREP
-template <int kBlocks, int kExt>
-__device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &sh, int32_t r,
-                                             int32_t k, uint64_t ent0, int32_t my_slot,
-                                             const uint32_t (&ssrc)[kPvMaxInbox], bool jrep,
-                                             uint32_t pcol, bool pok, RowOut &ro, PvMark &pm) {
-    constexpr int Q = kBlocks;                           // keys per lane
+template <int kBlocks, int kExt, int NT, class Sh>
+__device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int32_t r,
+                                             int32_t k, const uint64_t (&ent0)[kSlots / NT],
+                                             int32_t my_slot, const uint32_t (&ssrc)[kPvMaxInbox],
+                                             bool jrep, uint32_t pcol, bool pok, RowOut &ro,
+                                             PvMark &pm) {
+    constexpr int SL = kSlots / NT;                      // slots of each source per lane
+    constexpr int Q = kBlocks * SL;                      // keys per lane
     constexpr int kJ = kBlocks - 1;                      // k <= kJ messages in this variant
     constexpr int P = kBlocks * kSlots;
+    static_assert(P <= int(sizeof(sh.vals) / 2), "row LDS too small for this variant");
     const int32_t tid = threadIdx.x;
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
@@ -237,70 +248,99 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     // ---- 2. keys: one sorted block of 256 slots per source ------------------------------------
     // block 0 = the own view (loaded with the record), block m = message m's payload: the
     // sender's view (one coalesced 2 KB load) cut to what it gossiped at t - 1 (TFAIL), or for
-    // a JOINREP node 0's view cut to the Philox-chosen members (bounded introducer list)
+    // a JOINREP node 0's view cut to the Philox-chosen members (bounded introducer list).
+    // Lane tid holds slots [tid * SL, tid * SL + SL) of every block.
     const uint32_t tf = uint32_t(a.tfail), t5m1 = (t - 1u) & 31u;
     auto gossiped = [&](uint64_t v) {      // listed, and not suspected when sent at t - 1
         return v != kPvEmpty && (tf == 0 || ((t5m1 - uint32_t(v)) & 31u) < tf);
     };
-    uint64_t ent[kBlocks];
-    ent[0] = ent0;
+    uint64_t ent[kBlocks][SL];
+#pragma unroll
+    for (int i = 0; i < SL; ++i) ent[0][i] = ent0[i];
 #pragma unroll
     for (int m = 1; m < kBlocks; ++m) {
-        ent[m] = kPvEmpty;
-        if (m <= k && tid < V) {
+#pragma unroll
+        for (int i = 0; i < SL; ++i) ent[m][i] = kPvEmpty;
+        if (m <= k) {
             const int32_t sl = __builtin_amdgcn_readlane(my_slot, m - 1);
             const uint64_t *row = (m == 1 && jrep) ? a.intro
                                   : sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
-            ent[m] = __builtin_nontemporal_load(row + tid);
-            if ((kExt & kExtPol) && !gossiped(ent[m])) ent[m] = kPvEmpty;
+#pragma unroll
+            for (int i = 0; i < SL; ++i) {
+                const int32_t slot = tid * SL + i;
+                if (slot < V) {
+                    ent[m][i] = __builtin_nontemporal_load(row + slot);
+                    if ((kExt & kExtPol) && !gossiped(ent[m][i])) ent[m][i] = kPvEmpty;
+                }
+            }
         }
     }
     if constexpr (kBlocks > 1 && (kExt & kExtPol)) if (jrep) {   // block-uniform: node 0's gossiped members
-        const bool g = ent[1] != kPvEmpty;
+        uint32_t gl = 0;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) gl += ent[1][i] != kPvEmpty ? 1u : 0u;
         uint32_t cnt0 = 0;
-        const uint32_t rank = block_scan(g ? 1u : 0u, &cnt0, sh.keys[1]);   // keys[1] is free here
+        uint32_t rank = block_scan<NT>(gl, &cnt0, sh.keys[1]);   // keys[1] is free here
         const int32_t B = a.intro_list < int32_t(cnt0) ? a.intro_list : int32_t(cnt0);
         uint64_t cm[4];
         pv_intro_mask(a.seed, t - 1u, uint32_t(r), int32_t(cnt0), B, cm);
-        const uint32_t w = rank >> 6;
-        const uint64_t word = w == 0 ? cm[0] : w == 1 ? cm[1] : w == 2 ? cm[2] : cm[3];
-        if (!(g && ((word >> (rank & 63u)) & 1ull))) ent[1] = kPvEmpty;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const bool g = ent[1][i] != kPvEmpty;
+            const uint32_t w = rank >> 6;
+            const uint64_t word = w == 0 ? cm[0] : w == 1 ? cm[1] : w == 2 ? cm[2] : cm[3];
+            if (!(g && ((word >> (rank & 63u)) & 1ull))) ent[1][i] = kPvEmpty;
+            rank += g ? 1u : 0u;
+        }
     }
     // A TFAIL- or introducer-filtered payload has holes: its keys are compacted to the front
     // of the block (the tree merges sorted blocks).  Block-uniform; one scan per message.
-    int32_t kpos[kBlocks];                               // slot of this lane's key
-    uint32_t kpad = 0;                                   // bit m: lane pads its own slot of block m
+    int32_t kpos[kBlocks][SL];                           // slot of this lane's keys
+    uint32_t kpad = 0;                                   // bit m * SL + i: slot i is padding
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
-        kpos[m] = tid;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) kpos[m][i] = tid * SL + i;
         if ((kExt & kExtPol) && m >= 1 && (tf != 0 || (m == 1 && jrep)) && m <= k) {
-            const bool ok = ent[m] != kPvEmpty;
+            uint32_t cl = 0;
+#pragma unroll
+            for (int i = 0; i < SL; ++i) cl += ent[m][i] != kPvEmpty ? 1u : 0u;
             uint32_t cnt = 0;
-            const uint32_t pos = block_scan(ok ? 1u : 0u, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
-            kpos[m] = ok ? int32_t(pos) : -1;
-            kpad |= uint32_t(tid >= int32_t(cnt)) << m;
+            uint32_t pos = block_scan<NT>(cl, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
+#pragma unroll
+            for (int i = 0; i < SL; ++i) {
+                const bool ok = ent[m][i] != kPvEmpty;
+                kpos[m][i] = ok ? int32_t(pos) : -1;
+                pos += ok ? 1u : 0u;
+                kpad |= uint32_t(tid * SL + i >= int32_t(cnt)) << (m * SL + i);
+            }
         }
     }
     uint32_t merged = 0;                                 // payload entries (MP1Node.cpp:245 trips)
 #pragma unroll
     for (int m = 0; m < kBlocks; ++m) {
-        const bool ok = ent[m] != kPvEmpty;
-        merged += (m >= 1 && ok) ? 1u : 0u;
-        if ((kExt & kExtPol) && ((kpad >> m) & 1u)) sh.keys[0][m * kSlots + tid] = kKeyMax;   // compacted tail
-        if (!(kExt & kExtPol) || kpos[m] >= 0)
-            sh.keys[0][m * kSlots + kpos[m]] =
-                ok ? (uint32_t(ent[m] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(tid) : kKeyMax;
-        sh.vals[m * kSlots + tid] = uint16_t(ent[m]);
-        if (m > k) sh.keys[1][m * kSlots + tid] = kKeyMax;     // padding for the ping-pong
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const int32_t slot = tid * SL + i;
+            const bool ok = ent[m][i] != kPvEmpty;
+            merged += (m >= 1 && ok) ? 1u : 0u;
+            if ((kExt & kExtPol) && ((kpad >> (m * SL + i)) & 1u)) sh.keys[0][m * kSlots + slot] = kKeyMax;
+            if (!(kExt & kExtPol) || kpos[m][i] >= 0)
+                sh.keys[0][m * kSlots + kpos[m][i]] =
+                    ok ? (uint32_t(ent[m][i] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(slot) : kKeyMax;
+            sh.vals[m * kSlots + slot] = uint16_t(ent[m][i]);
+            if (m > k) sh.keys[1][m * kSlots + slot] = kKeyMax;     // padding for the ping-pong
+        }
     }
     __syncthreads();
     pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
     // Level s merges neighbouring segments of s keys (the last one of a level may be shorter
-    // or alone when kBlocks is not a power of two).  The tree hands out Qt = 2^ceil(log2 Q)
-    // outputs per lane, so a lane's outputs never straddle two merges (P / Qt lanes work).
-    constexpr int Qt = Q <= 2 ? Q : Q <= 4 ? 4 : 8;   // 8 or 16 for Q <= 4: +1 % / +6 %
+    // or alone when kBlocks is not a power of two).  The tree hands out Qt = 2^ceil(log2
+    // kBlocks) * SL outputs per lane, so a lane's outputs never straddle two merges (P / Qt
+    // lanes work).
+    constexpr int Qt = (kBlocks <= 2 ? kBlocks : kBlocks <= 4 ? 4 : 8) * SL;
     constexpr bool kPow2 = (kBlocks & (kBlocks - 1)) == 0;
     const int32_t begt = tid * Qt;
     int cur = 0;
@@ -318,44 +358,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 sb = rest - s < s ? (rest > s ? rest - s : 0) : s;
             }
             int32_t lo = o > sb ? o - sb : 0, hi = o < sa ? o : sa;
-#if GSP_PV_CORANK4
-            while (lo < hi) {                                  // co-rank of output o, 4-ary:
-                const int32_t len = hi - lo;                   // three independent probes a step
-                const int32_t m1 = lo + (len >> 2), m2 = lo + (len >> 1), m3 = lo + ((3 * len) >> 2);
-                const bool f1 = A[m1] < B[o - m1 - 1], f2 = A[m2] < B[o - m2 - 1],
-                           f3 = A[m3] < B[o - m3 - 1];
-                if (f3) lo = m3 + 1;
-                else if (f2) { lo = m2 + 1; hi = m3; }
-                else if (f1) { lo = m1 + 1; hi = m2; }
-                else hi = m1;
-            }
-#else
             while (lo < hi) {                                  // co-rank of output o
                 const int32_t mid = (lo + hi) >> 1;
                 if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
             }
-#endif
             int32_t i = lo, j = o - lo;
             uint32_t outk[Qt];
-#if GSP_PV_TREE_WIN
-            // the next Qt keys of each side (independent loads), then the Qt smallest of the
-            // two windows: min(A[e], B[Qt-1-e]) is bitonic, and a half-cleaner network sorts it
-#pragma unroll
-            for (int e = 0; e < Qt; ++e) {
-                const uint32_t wa = i + e < sa ? A[i + e] : kKeyMax;
-                const uint32_t wb = j + (Qt - 1 - e) < sb ? B[j + (Qt - 1 - e)] : kKeyMax;
-                outk[e] = wa < wb ? wa : wb;
-            }
-#pragma unroll
-            for (int d = Qt / 2; d >= 1; d >>= 1)
-#pragma unroll
-                for (int e = 0; e < Qt; ++e)
-                    if ((e & d) == 0) {
-                        const uint32_t x = outk[e], y = outk[e + d];
-                        outk[e] = x < y ? x : y;
-                        outk[e + d] = x < y ? y : x;
-                    }
-#else
             uint32_t va = i < sa ? A[i] : kKeyMax, vb = j < sb ? B[j] : kKeyMax;
 #pragma unroll
             for (int e = 0; e < Qt; ++e) {
@@ -368,7 +376,6 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
                 va = ta ? nv : va;
                 vb = ta ? vb : nv;
             }
-#endif
             lds_store<Qt>(Y + begt, outk);
         }
         __syncthreads();
@@ -378,10 +385,11 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     const uint32_t *C = sh.keys[cur];
     // keys[cur ^ 1] (the last level's source) is dead after the tree: it holds the eviction
     // histogram over (age, hb) bins (1024 u16 counters at words [512, 1024)) and the scan
-    // buffers (words [2040, 2048))
+    // buffers (8 words at Sh::kScan)
     uint32_t *const bins = sh.keys[cur ^ 1] + kBinWord;
-    uint32_t *const scan_buf = sh.keys[cur ^ 1] + 2040;
-    reinterpret_cast<uint2 *>(bins)[tid] = make_uint2(0u, 0u);
+    uint32_t *const scan_buf = sh.keys[cur ^ 1] + Sh::kScan;
+#pragma unroll
+    for (int i = tid; i < 256; i += NT) reinterpret_cast<uint2 *>(bins)[i] = make_uint2(0u, 0u);
 
     pm.mark(2);
     // ---- 4. fold every id run that starts in this lane, in registers ------------------------
@@ -393,7 +401,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
     for (int e = 0; e < Q; ++e)                                // value gathers, all in flight
         vv[e] = ck[e] != kKeyMax ? uint32_t(sh.vals[key_src(ck[e]) * kSlots + key_slot(ck[e])]) : 0u;
     const uint32_t lo_id = tid > 0 ? key_id(prev_key) + 1u : 0u;   // this lane brackets ids
-    const uint32_t hi_id = tid < kPvBlock - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
+    const uint32_t hi_id = tid < NT - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
 
     uint32_t res[Q], rid[Q];
     uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
@@ -533,7 +541,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         }
     };
     uint32_t total = 0;
-    const uint32_t base = block_scan(nloc, &total, scan_buf);
+    const uint32_t base = block_scan<NT>(nloc, &total, scan_buf);
     const bool evict = int32_t(total) > V;
     if (!evict) {                                              // the survivors are the view
         uint32_t *Uid = sh.keys[cur ^ 1];
@@ -593,8 +601,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
         const uint32_t astar = bstar >> 5;
         uint32_t hstar = th0 - astar - (bstar & 31u), need2 = need;
         if (tie && (bstar & 31u) == 31u) {                               // block-uniform: exact hb boundary
-            uint32_t *hist = sh.keys[cur] + kHistWord;     // 2048 hb bins, u16 pairs; C is dead
-            for (int32_t i = tid; i < kMaxKeys / 2; i += kPvBlock) hist[i] = 0;
+            uint32_t *hist = sh.keys[cur] + Sh::kHist;     // 2048 hb bins, u16 pairs; C is dead
+            for (int32_t i = tid; i < 1024; i += NT) hist[i] = 0;
             __syncthreads();
             for_each([&](uint32_t v, uint32_t, uint32_t b) {
                 if (b == bstar)
@@ -636,7 +644,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
             nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
         });
         uint32_t sums = 0;
-        const uint32_t ex = block_scan(nt | (nk << 16), &sums, scan_buf + 4);
+        const uint32_t ex = block_scan<NT>(nt | (nk << 16), &sums, scan_buf + 4);
         uint32_t tie_before = ex & 0xFFFFu;
         const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
@@ -681,8 +689,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, PvShared &s
 // ---- 6. write the view and the row's digest record (peers: pview_send_kernel) -------------
 // rowdig[lr][wave][4]: w0 = merges | delivered << 32 | sent << 40 | dropped << 48 | round << 56,
 // w1 = joins | removes << 16 | evicts << 32 | overflow << 48, w2 = event hash, w3 = 0; each
-// wave writes its own partial record (no barrier); sent / dropped come from the send kernel.
-__device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, int32_t lr,
+// wave writes its own partial record (no barrier; a 128-lane row's two waves also zero the
+// records of waves 2 and 3); sent / dropped come from the send kernel.
+template <int NT, class Sh>
+__device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_t lr,
                                           int32_t k, int32_t k_all, bool init, const RowOut &ro) {
     const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int32_t V = a.view, len = ro.len;
@@ -690,7 +700,7 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
     const uint32_t *ids = &sh.keys[0][0] + ro.ids_off;
     const uint16_t *vals = reinterpret_cast<const uint16_t *>(&sh) + ro.vals_off;
     uint64_t *out = a.cur + int64_t(lr) * V;
-    for (int32_t i = tid; i < V; i += kPvBlock)
+    for (int32_t i = tid; i < V; i += NT)
         __builtin_nontemporal_store(
             i < len ? (uint64_t(ids[i]) << 32) | uint64_t(vals[i]) : kPvEmpty, out + i);
     if (init) {
@@ -718,14 +728,20 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, PvShared &sh, 
         rec[0] = make_ulonglong2(w0, w1);
         if (wave == 0) rec[1].x = h;                  // w3 belongs to the send kernel
         else rec[1] = make_ulonglong2(h, 0ull);
+        if (NT == 128) {
+            ulonglong2 *z = reinterpret_cast<ulonglong2 *>(a.rowdig + (int64_t(lr) * 4 + wave + 2) * 4);
+            z[0] = z[1] = make_ulonglong2(0ull, 0ull);
+        }
     }
 }
 
-// workgroup-order index b -> row: b itself, or the b-th row of the k-descending order
+// workgroup-order index b -> row: b itself, or the b-th row of the k-descending order of
+// the buckets k in [kQlo, kQhi]
+template <int kQlo = 0, int kQhi = 7>
 __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) {
     if (!a.order) return b;
-    int32_t q = 7;
-    for (; q > 0; --q) {
+    int32_t q = kQhi;
+    for (; q > kQlo; --q) {
         const int32_t c = a.kcount[q];
         if (b < c) break;
         b -= c;
@@ -735,12 +751,18 @@ __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) 
 
 // One non-init row: the own view slot and the receipt record are requested first (their
 // latencies overlap), then merge, ops, eviction, view write and digest record.
-template <int kExt>
-__device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int32_t lr) {
+// NT lanes per row; the row's k (merged messages) lies in [kQlo, kQhi] -- only those
+// variants are compiled in.
+template <int kExt, int NT, int kQlo, int kQhi, class Sh>
+__device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t lr) {
+    constexpr int SL = kSlots / NT;
     const int32_t tid = threadIdx.x, lane = tid & 63;
     const int32_t r = a.row0 + lr;
-    const uint64_t ent0 = tid < a.view ? __builtin_nontemporal_load(a.prev + int64_t(lr) * a.view + tid)
-                                       : kPvEmpty;
+    uint64_t ent0[SL];
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        ent0[i] = tid * SL + i < a.view ? __builtin_nontemporal_load(a.prev + int64_t(lr) * a.view + tid * SL + i)
+                                        : kPvEmpty;
     const int32_t info_v = a.rc_info[lr];
     const int32_t my_src = lane < 8 ? a.rc_src[int64_t(lr) * 8 + lane] : 0;
     const int32_t my_slot = lane < 8 ? a.rc_slot[int64_t(lr) * 8 + lane] : 0;
@@ -777,23 +799,23 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, PvShared &sh, int
     }
     pm.mark(0);
     // one variant per key count (own view + k sender views)
-    if (k == 0) pv_merge_row<1, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 1) pv_merge_row<2, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 2) pv_merge_row<3, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 3) pv_merge_row<4, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 4) pv_merge_row<5, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 5) pv_merge_row<6, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else if (k == 6) pv_merge_row<7, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
-    else pv_merge_row<8, kExt>(a, sh, r, k, ent0, my_slot, ssrc, jrep, pcol, pok, ro, pm);
+#define GSP_PV_VARIANT(K)                                                                        \
+    else if (kQlo <= K && K <= kQhi && k == K)                                                  \
+        pv_merge_row<(K < kQlo ? kQlo : K > kQhi ? kQhi : K) + 1, kExt, NT>(a, sh, r, k, ent0, my_slot, \
+                                                                          ssrc, jrep, pcol, pok, ro, pm);
+    if (false) {}
+    GSP_PV_VARIANT(0) GSP_PV_VARIANT(1) GSP_PV_VARIANT(2) GSP_PV_VARIANT(3)
+    GSP_PV_VARIANT(4) GSP_PV_VARIANT(5) GSP_PV_VARIANT(6) GSP_PV_VARIANT(7)
+#undef GSP_PV_VARIANT
     pm.mark(5);
-    pv_finish(a, sh, lr, k, k_all, false, ro);
+    pv_finish<NT>(a, sh, lr, k, k_all, false, ro);
     pm.mark(6);
 }
 
 // Tick 0: every row writes its pre-joined bounded view {(r + 1 + j * (n / V)) mod n} (or
 // everyone if n - 1 <= V) with hb = h0, ts = 0.
 __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
-    __shared__ PvShared sh;
+    __shared__ PvShared<kMaxKeys> sh;
     const int32_t tid = threadIdx.x;
     const int32_t lr = blockIdx.x, r = a.row0 + lr, V = a.view, n = a.n;
     if (a.tick > a.fail_tick[r]) {
@@ -833,7 +855,7 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
     for (int32_t i = tid; i < ro.len; i += kPvBlock) sh.vals[i] = uint16_t(a.h0 << 5);
     ro.vals_off = lds_half(sh, sh.vals);
     __syncthreads();
-    pv_finish(a, sh, lr, 0, 0, true, ro);
+    pv_finish<kPvBlock>(a, sh, lr, 0, 0, true, ro);
 }
 
 // kWaves: minimum waves per SIMD the register allocation must allow (8 = 8 rows per CU, the
@@ -843,8 +865,26 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
 // -- other resident rows already hide the HBM round trips.
 template <int kWaves, int kExt>
 __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
-    __shared__ PvShared sh;
-    pv_row<kExt>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
+    __shared__ PvShared<kMaxKeys> sh;
+    pv_row<kExt, kPvBlock, 0, 7>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
+}
+
+// Split form (rows bucketed by k, a.order set): the rows that merge at most 3 messages
+// (kQhi = 3: at most 4 sources, 1024 keys) run as 128-lane rows in 10 KB of LDS -- 16 rows
+// per CU instead of 8, two waves per row instead of four, each lane holding two slots of
+// every source -- and the rest as 256-lane rows.  The bucket sizes are on the device, so
+// each kernel is launched over every row and the workgroups past its buckets' rows return
+// at once (a grid-stride loop instead kept the row body's loop-invariant values live across
+// it and spilled).
+template <int kExt, int NT, int kQlo, int kQhi>
+__global__ void __launch_bounds__(NT, 8) pview_tick_split_kernel(PviewTickArgs a) {
+    __shared__ PvShared<kQhi <= 3 ? 1024 : kMaxKeys> sh;
+    int32_t total = 0;
+#pragma unroll
+    for (int q = kQlo; q <= kQhi; ++q) total += a.kcount[q];
+    const int32_t b = int32_t(blockIdx.x);
+    if (b >= total) return;
+    pv_row<kExt, NT, kQlo, kQhi>(a, sh, pv_row_of<kQlo, kQhi>(a, b));
 }
 
 // One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
@@ -1071,6 +1111,30 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     // kExtEv for the event stream (the plain protocol runs neither)
     const int ext = ((a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr) ? kExtPol : 0) |
                     (a.ev.buf != nullptr ? kExtEv : 0);
+    if (a.order && a.split) {
+        // split form: rows with k >= 4 as 256-lane rows, k <= 3 as 128-lane rows
+        const unsigned gb = unsigned(a.rows), gs = unsigned(a.rows);
+        switch (ext) {
+            case 0:
+                hipLaunchKernelGGL((pview_tick_split_kernel<0, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((pview_tick_split_kernel<0, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
+                break;
+            case kExtEv:
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtEv, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtEv, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
+                break;
+            case kExtPol:
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
+                break;
+            default:
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol | kExtEv, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
+                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol | kExtEv, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
+                break;
+        }
+        launch_send_and_digest(a, st);
+        return hipGetLastError();
+    }
     const bool w8 = a.waves == 8;
     switch (ext) {
         case 0: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, 0>), g, blk, 0, st, a);

@@ -57,6 +57,7 @@ struct PviewTickArgs {
                                  // of the k-descending order (one code variant per CU stretch)
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
     int32_t waves;               // register budget variant of the tick kernel (7 or 8)
+    int32_t split;               // with order set: k <= 3 rows as 128-lane rows (two kernels)
 };
 constexpr int kPvProfPhases = 10;
 

@@ -139,11 +139,15 @@ def test_pview_rccl_one_rank():
 def test_pview_capacity_error_stops_the_job(monkeypatch):
     """A receiver sent more messages than the receipt bound (1,024; lowered to 2 through the
     test-only GSP_TEST_MAX_SEGMENT) stops the job at that tick: its tick kernel and every later
-    one run no row, and the next step call and every read return GSP_ERR_CAPACITY."""
+    one run no row.  The flag reaches the host by an async copy at the end of each step call:
+    sync() (and every read) reports it, and so does every step call made after the copy
+    landed -- never state computed from a skipped row."""
     from gossip_protocol_amd._lib import GspError
     monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
     with PviewEngine(300, view=64, fanout=8, inbox=7, max_ticks=10) as eng:
         eng.step(1)
+        with pytest.raises(GspError, match="more than 2 messages at tick 1"):
+            eng.sync()
         with pytest.raises(GspError, match="more than 2 messages at tick 1"):
             eng.step(1)
         with pytest.raises(GspError, match="at tick 1"):

@@ -309,13 +309,16 @@ def test_scale_full_size_properties():
 def test_capacity_error_stops_the_job(monkeypatch):
     """A receiver sent more messages than the kernel's segment bound (1,024; lowered to 2 here
     through the test-only GSP_TEST_MAX_SEGMENT) stops the job loudly: the device flags the
-    tick, every later tick kernel runs no row, and the next gsp_scale_step call (no host
-    synchronisation needed) and every read return GSP_ERR_CAPACITY instead of state computed
-    from a skipped row."""
+    tick and every later tick kernel runs no row.  The flag reaches the host by an async copy
+    at the end of each step call: sync() and every read return GSP_ERR_CAPACITY, and so does
+    every gsp_scale_step call made after the copy landed -- never state computed from a
+    skipped row."""
     from gossip_protocol_amd._lib import GspError
     monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
     with ScaleEngine(256, fanout=8, max_ticks=10) as eng:
         eng.step(1)                      # tick 1: ~8 messages per receiver > 2
+        with pytest.raises(GspError, match="more than 2 messages at tick 1"):
+            eng.sync()
         with pytest.raises(GspError, match="more than 2 messages at tick 1"):
             eng.step(1)
         with pytest.raises(GspError, match="at tick 1"):
