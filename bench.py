@@ -254,7 +254,8 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "xgmi_bytes_per_tick": xgmi, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
-                     "kernel": "pview_tick_kernel", "valu": _pview_valu(nodes, world, kern_ms),
+                     "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
+                     "valu": _pview_valu(nodes, world, kern_ms),
                      "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
     }
     if world == 1 and cpu_baseline_on:

@@ -1113,25 +1113,27 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
                     (a.ev.buf != nullptr ? kExtEv : 0);
     if (a.order && a.split) {
         // split form: rows with k >= 4 as 256-lane rows, k <= 3 as 128-lane rows
-        const unsigned gb = unsigned(a.rows), gs = unsigned(a.rows);
-        switch (ext) {
-            case 0:
-                hipLaunchKernelGGL((pview_tick_split_kernel<0, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
-                hipLaunchKernelGGL((pview_tick_split_kernel<0, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
-                break;
-            case kExtEv:
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtEv, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtEv, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
-                break;
-            case kExtPol:
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
-                break;
-            default:
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol | kExtEv, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a);
-                hipLaunchKernelGGL((pview_tick_split_kernel<kExtPol | kExtEv, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a);
-                break;
+        unsigned gb = unsigned(a.rows), gs = unsigned(a.rows);
+        if (a.kcount_host) {                          // exact grids: the counts, synchronously
+            if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return hipGetLastError();
+            gb = unsigned(a.kcount_host[4] + a.kcount_host[5] + a.kcount_host[6] + a.kcount_host[7]);
+            gs = unsigned(a.kcount_host[0] + a.kcount_host[1] + a.kcount_host[2] + a.kcount_host[3]);
         }
+        auto launch = [&](auto big, auto small) {     // small rows first with split = 2
+            if (a.split == 2) { small(); big(); } else { big(); small(); }
+        };
+#define GSP_PV_SPLIT_LAUNCH(E)                                                                        \
+    launch([&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a); }, \
+           [&] { if (gs) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a); })
+        switch (ext) {
+            case 0: GSP_PV_SPLIT_LAUNCH(0); break;
+            case kExtEv: GSP_PV_SPLIT_LAUNCH(kExtEv); break;
+            case kExtPol: GSP_PV_SPLIT_LAUNCH(kExtPol); break;
+            default: GSP_PV_SPLIT_LAUNCH(kExtPol | kExtEv); break;
+        }
+#undef GSP_PV_SPLIT_LAUNCH
         launch_send_and_digest(a, st);
         return hipGetLastError();
     }

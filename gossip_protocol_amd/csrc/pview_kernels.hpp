@@ -58,6 +58,8 @@ struct PviewTickArgs {
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
     int32_t waves;               // register budget variant of the tick kernel (7 or 8)
     int32_t split;               // with order set: k <= 3 rows as 128-lane rows (two kernels)
+    int32_t *kcount_host;        // pinned [8], or null: the split kernels' grids are the exact
+                                 // bucket sizes, read back with a stream sync (A/B: GSP_PV_SPLITSYNC)
 };
 constexpr int kPvProfPhases = 10;
 

@@ -33,5 +33,6 @@ step pv_sq 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_IN
 cd "$GRAFT_REPO_ROOT"
 python3 scripts/pmc_traffic.py $(ls "$OUT"/pmc_fetch/*counter_collection.csv) $(ls "$OUT"/pmc_write/*counter_collection.csv) "$OUT/pmc_traffic.json" --tiles 8
 python3 scripts/pmc_traffic.py $(ls "$OUT"/pv_fetch/*counter_collection.csv) $(ls "$OUT"/pv_write/*counter_collection.csv) "$OUT/pmc_traffic_pview.json" --pview
-python3 scripts/pmc_summary.py "pview_tick_kernel<8, 0>" $(ls "$OUT"/pv_sq/*counter_collection.csv) --json "$OUT/pmc_sq_pview.json"
+python3 scripts/pmc_summary.py "pview_tick_split_kernel<0, " $(ls "$OUT"/pv_sq/*counter_collection.csv) \
+    --per-tick "pview_tick_split_kernel<0, 128" --json "$OUT/pmc_sq_pview.json"
 echo done

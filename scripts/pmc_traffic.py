@@ -3,8 +3,8 @@
 
     python scripts/pmc_traffic.py <pmc_fetch.csv> <pmc_write.csv> [out.json] [--pview] [--tiles T]
 
---pview: the partial-view tick kernel (8-B/lane view loads and stores) instead of the
-full-view fused tick kernel.  --tiles T: the full view ran as T column tiles (T launches per
+--pview: the partial-view tick kernels (8-B/lane view loads and stores; per tick the
+256-lane and the 128-lane split kernel, summed) instead of the full-view fused tick kernel.  --tiles T: the full view ran as T column tiles (T launches per
 tick); bytes_per_tick = T x the per-launch average.
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts half of
@@ -20,19 +20,27 @@ KERNEL = "scale_tick_kernel<false"
 NOTE = "FETCH_SIZE x2 (gfx950 counts half of 16-B/lane streaming reads)"
 
 
+ANCHOR = None   # --pview: one dispatch of this kernel per tick; the tick's kernels are summed
+
+
 def per_launch(path, counter):
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    return sum(vals) / len(vals), len(vals)
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    vals = [float(r["Counter_Value"]) for r in rows if KERNEL in r["Kernel_Name"]]
+    if ANCHOR is None:
+        return sum(vals) / len(vals), len(vals)
+    ticks = sum(1 for r in rows if ANCHOR in r["Kernel_Name"])
+    return sum(vals) / ticks, ticks
 
 
 def main():
-    global KERNEL, NOTE
+    global KERNEL, NOTE, ANCHOR
     name = "scale_tick_kernel (fused merge/ops/send)"
     if "--pview" in sys.argv:
         sys.argv.remove("--pview")
-        KERNEL = "pview_tick_kernel<8, 0>"
-        name = "pview_tick_kernel (partial-view union/fold/evict)"
+        KERNEL = "pview_tick_split_kernel<0, "
+        ANCHOR = "pview_tick_split_kernel<0, 128"
+        name = ("pview_tick_split_kernel (partial-view union/fold/evict; per tick: the 256-lane and "
+                "the 128-lane kernel summed)")
         NOTE = ("FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
                 "loads: uncalibrated for that width, MI355X_MICROARCH.md HBM section)")
     tiles = 1
