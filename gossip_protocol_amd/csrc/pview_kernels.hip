@@ -151,8 +151,8 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
 // when no eviction is needed, the survivor ids U (words [0, 256)).
 template <int kKeys>
 struct alignas(16) PvShared {
-    static_assert(kKeys == 1024 || kKeys == 2048, "one or two 1024-key halves");
-    static constexpr int kHist = kKeys - 1024, kScan = kKeys == 2048 ? 2040 : 504;
+    static_assert(kKeys >= 1024 && kKeys <= 2048 && kKeys % 256 == 0, "4 to 8 sources of 256 keys");
+    static constexpr int kHist = kKeys - 1024, kScan = kKeys > 1024 ? kKeys - 8 : 504;
     uint32_t keys[2][kKeys];             // merge ping-pong; then the regions above
     uint16_t vals[kKeys];                // values by (source, slot); then survivor values
 };
@@ -876,9 +876,9 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
 // each kernel is launched over every row and the workgroups past its buckets' rows return
 // at once (a grid-stride loop instead kept the row body's loop-invariant values live across
 // it and spilled).
-template <int kExt, int NT, int kQlo, int kQhi>
-__global__ void __launch_bounds__(NT, 8) pview_tick_split_kernel(PviewTickArgs a) {
-    __shared__ PvShared<kQhi <= 3 ? 1024 : kMaxKeys> sh;
+template <int kExt, int NT, int kQlo, int kQhi, int kMinWaves = 8>
+__global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTickArgs a) {
+    __shared__ PvShared<kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots> sh;
     int32_t total = 0;
 #pragma unroll
     for (int q = kQlo; q <= kQhi; ++q) total += a.kcount[q];
@@ -1113,19 +1113,35 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
                     (a.ev.buf != nullptr ? kExtEv : 0);
     if (a.order && a.split) {
         // split form: rows with k >= 4 as 256-lane rows, k <= 3 as 128-lane rows
-        unsigned gb = unsigned(a.rows), gs = unsigned(a.rows);
+        unsigned gb = unsigned(a.rows), gs = unsigned(a.rows), g4 = unsigned(a.rows), g5 = unsigned(a.rows),
+                 g67 = unsigned(a.rows);
         if (a.kcount_host) {                          // exact grids: the counts, synchronously
             if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return hipGetLastError();
-            gb = unsigned(a.kcount_host[4] + a.kcount_host[5] + a.kcount_host[6] + a.kcount_host[7]);
-            gs = unsigned(a.kcount_host[0] + a.kcount_host[1] + a.kcount_host[2] + a.kcount_host[3]);
+            const int32_t *c = a.kcount_host;
+            gb = unsigned(c[4] + c[5] + c[6] + c[7]);
+            gs = unsigned(c[0] + c[1] + c[2] + c[3]);
+            g4 = unsigned(c[4]);
+            g5 = unsigned(c[5]);
+            g67 = unsigned(c[6] + c[7]);
         }
-        auto launch = [&](auto big, auto small) {     // small rows first with split = 2
-            if (a.split == 2) { small(); big(); } else { big(); small(); }
+        // split bits: 1 on, 2 small rows first, 4 the k >= 4 rows as 128-lane rows too (20 KB
+        // of LDS: 8 rows, 4 waves per SIMD, up to 128 VGPRs), 8 the k = 4 and k = 5 rows as
+        // 128-lane rows in 12.5 / 15 KB (12 / 10 rows per CU) and k = 6, 7 as 256-lane rows
+        auto launch = [&](auto big, auto big128, auto k4, auto k5, auto k67, auto small) {
+            if (a.split & 2) small();
+            if (a.split & 8) { k67(); k5(); k4(); }
+            else if (a.split & 4) big128();
+            else big();
+            if (!(a.split & 2)) small();
         };
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                        \
     launch([&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a); }, \
+           [&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 7, 4>), dim3(gb), dim3(128), 0, st, a); }, \
+           [&] { if (g4) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(g4), dim3(128), 0, st, a); }, \
+           [&] { if (g5) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(g5), dim3(128), 0, st, a); }, \
+           [&] { if (g67) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(g67), dim3(256), 0, st, a); }, \
            [&] { if (gs) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a); })
         switch (ext) {
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
