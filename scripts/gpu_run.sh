@@ -34,5 +34,5 @@ cd "$GRAFT_REPO_ROOT"
 python3 scripts/pmc_traffic.py $(ls "$OUT"/pmc_fetch/*counter_collection.csv) $(ls "$OUT"/pmc_write/*counter_collection.csv) "$OUT/pmc_traffic.json" --tiles 8
 python3 scripts/pmc_traffic.py $(ls "$OUT"/pv_fetch/*counter_collection.csv) $(ls "$OUT"/pv_write/*counter_collection.csv) "$OUT/pmc_traffic_pview.json" --pview
 python3 scripts/pmc_summary.py "pview_tick_split_kernel<0, " $(ls "$OUT"/pv_sq/*counter_collection.csv) \
-    --per-tick "pview_tick_split_kernel<0, 128" --json "$OUT/pmc_sq_pview.json"
+    --per-tick "pview_tick_split_kernel<0, 128, 0, 3," --json "$OUT/pmc_sq_pview.json"
 echo done

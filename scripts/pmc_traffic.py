@@ -38,7 +38,7 @@ def main():
     if "--pview" in sys.argv:
         sys.argv.remove("--pview")
         KERNEL = "pview_tick_split_kernel<0, "
-        ANCHOR = "pview_tick_split_kernel<0, 128"
+        ANCHOR = "pview_tick_split_kernel<0, 128, 0, 3,"
         name = ("pview_tick_split_kernel (partial-view union/fold/evict; per tick: the 256-lane and "
                 "the 128-lane kernel summed)")
         NOTE = ("FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
