@@ -75,7 +75,7 @@ struct gsp_pview {
     int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
     int32_t split = 9;           // GSP_PV_SPLIT bits (pview_kernels.hip): 1 rows merging <= 3
                                  // messages as 128-lane rows, 8 also k = 4, 5 in their own kernels
-                                 // (2 small rows first, 4 every row 128 lanes; 0: one kernel)
+                                 // (2 small rows first, 32 k = 0 rows alone; 0: one kernel)
     bool split_sync = true;      // exact split grids from the counts read back, one stream sync
                                  // per tick (GSP_PV_SPLITSYNC=0: grids of every row, the rows past a
                                  // bucket range return at once; A/B 6.14 vs 5.95 ms per tick)

@@ -1128,28 +1128,23 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
             g0 = unsigned(c[0]);
             g13 = unsigned(c[1] + c[2] + c[3]);
         }
-        // split bits: 1 on, 2 small rows first, 4 the k >= 4 rows as 128-lane rows too (20 KB
-        // of LDS: 8 rows, 4 waves per SIMD, up to 128 VGPRs), 8 the k = 4 and k = 5 rows as
-        // 128-lane rows in 12.5 / 15 KB (12 / 10 rows per CU) and k = 6, 7 as 256-lane rows
-        // (16: k = 6, 7 as 128-lane rows in 20 KB), 32 the k = 0 rows in a kernel of their own.
-        // A/B (ticks 6-15, one box): 1 -> 9 -1.6 %, 4 +8.7 %, 25 +6 %, 41 -0.7 %; a one-wave
-        // k = 0 kernel without LDS (scan + compaction only) measured +7 % and was dropped.
-        auto launch = [&](auto big, auto big128, auto k4, auto k5, auto k67, auto k67n, auto small,
-                          auto k0, auto k13) {
+        // split bits: 1 on, 2 small rows first, 8 the k = 4 and k = 5 rows as 128-lane rows in
+        // 12.5 / 15 KB (12 / 10 rows per CU) and k = 6, 7 as 256-lane rows, 32 the k = 0 rows in
+        // a kernel of their own.  A/B (ticks 6-15, one box): 1 -> 9 -1.6 %, 41 -0.7 %; dropped:
+        // every k >= 4 row as a 128-lane row in 20 KB (8 rows, 4 waves per SIMD) +8.7 %, only
+        // k = 6, 7 so +6 %, a one-wave k = 0 kernel without LDS (scan + compaction) +7 %.
+        auto launch = [&](auto big, auto k4, auto k5, auto k67, auto small, auto k0, auto k13) {
             auto sm = [&] { if (a.split & 32) { k13(); k0(); } else small(); };
             if (a.split & 2) sm();
-            if (a.split & 8) { if (a.split & 16) k67n(); else k67(); k5(); k4(); }
-            else if (a.split & 4) big128();
+            if (a.split & 8) { k67(); k5(); k4(); }
             else big();
             if (!(a.split & 2)) sm();
         };
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                        \
     launch([&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a); }, \
-           [&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 7, 4>), dim3(gb), dim3(128), 0, st, a); }, \
            [&] { if (g4) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(g4), dim3(128), 0, st, a); }, \
            [&] { if (g5) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(g5), dim3(128), 0, st, a); }, \
            [&] { if (g67) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(g67), dim3(256), 0, st, a); }, \
-           [&] { if (g67) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 6, 7, 4>), dim3(g67), dim3(128), 0, st, a); }, \
            [&] { if (gs) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a); }, \
            [&] { if (g0) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 0>), dim3(g0), dim3(128), 0, st, a); }, \
            [&] { if (g13) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 1, 3>), dim3(g13), dim3(128), 0, st, a); })
