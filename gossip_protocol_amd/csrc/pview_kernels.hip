@@ -1132,7 +1132,8 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         // 12.5 / 15 KB (12 / 10 rows per CU) and k = 6, 7 as 256-lane rows, 32 the k = 0 rows in
         // a kernel of their own.  A/B (ticks 6-15, one box): 1 -> 9 -1.6 %, 41 -0.7 %; dropped:
         // every k >= 4 row as a 128-lane row in 20 KB (8 rows, 4 waves per SIMD) +8.7 %, only
-        // k = 6, 7 so +6 %, a one-wave k = 0 kernel without LDS (scan + compaction) +7 %.
+        // k = 6, 7 so +6 %, a one-wave k = 0 kernel without LDS (scan + compaction) +7 %, the
+        // k >= 4 kernels on a second stream beside the small rows' (fork / join events) ±0.5 %.
         auto launch = [&](auto big, auto k4, auto k5, auto k67, auto small, auto k0, auto k13) {
             auto sm = [&] { if (a.split & 32) { k13(); k0(); } else small(); };
             if (a.split & 2) sm();
