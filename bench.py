@@ -132,7 +132,8 @@ def cpu_baseline(budget_s=12.0):
     entries processed per second is converted to node-rounds/s of the 65,536-wide workload
     (a node-round there processes 65,536 x (1 + k) entries, k = messages merged).
     """
-    from tests.oracle_binding import ScaleOracle
+    from tests.oracle_binding import ScaleOracle, load_oracle
+    load_oracle().gsp_oracle_set_threads(1)        # the single-threaded restatement
     n = 4096
     orc = ScaleOracle(n, fanout=FANOUT, drop_pct=0, fail_mode=1, fail_tick=FAIL_TICK,
                       fail_ppm=FAIL_PPM, seed=SEED)
@@ -218,7 +219,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     launches = max(p1["merge_launches"] - p0["merge_launches"], 1)
     kern_ms = (p1["merge_ms"] - p0["merge_ms"]) / launches
     xch_ms = (p1["csr_ms"] - p0["csr_ms"]) / launches
-    bytes_per_launch = ((2.0 * rounds + delivered) * V * 8.0 + csr * 4.0) / steps
+    bytes_per_tick = ((2.0 * rounds + delivered) * V * 8.0 + csr * 4.0) / steps
     xgmi = (p1["xgmi_bytes"] - p0["xgmi_bytes"]) / steps
     ev = None
     if events:
@@ -230,17 +231,17 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     if dist is not None:
         t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device=_dev())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        u = torch.tensor([rounds, merges, bytes_per_launch, xgmi], dtype=torch.float64,
+        u = torch.tensor([rounds, merges, bytes_per_tick, xgmi], dtype=torch.float64,
                          device=_dev())
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         el, kern_ms, xch_ms = (x.item() for x in t)
-        rounds, merges, bytes_per_launch, xgmi = (x.item() for x in u)
+        rounds, merges, bytes_per_tick, xgmi = (x.item() for x in u)
         if dist.get_rank() != 0:
             return None
     if events:
         ev.update({"kinds": events, "kernel_ms": kern_ms, "value_events_on": rounds / el})
         return ev
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    achieved = bytes_per_tick / (kern_ms * 1e-3) / 1e9
     peak = PEAK_HBM_GBS * world
     out = {
         "metric": "gossip node-rounds/sec (partial view)", "value": rounds / el,
@@ -256,7 +257,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
                      "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
                      "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
                      "valu": _pview_valu(nodes, world, kern_ms),
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_per_launch},
+                     "kernel_ms_per_tick": kern_ms, "algorithmic_bytes_per_tick": bytes_per_tick},
     }
     if world == 1 and cpu_baseline_on:
         out["cpu_baseline"] = pview_cpu_baseline()
@@ -295,8 +296,18 @@ def _pview_valu(nodes, world, kern_ms):
 
 
 EVENT_CAP = 1 << 27          # records per shard (1 GB): config 3 records 70.7 M joins + removes
-TILES = 8                    # one GPU: config 3 as 8 column tiles of 8,192 columns (DESIGN.md
-                             # "Column tiles": 6.6 vs 8.0 ms per tick for the fused row kernel)
+TILE_COLS = 8192             # column tiles of 8,192 columns: config 3 as 8 tiles on one GPU
+                             # (DESIGN.md "Column tiles": 6.6 vs 8.0 ms per tick for the fused
+                             # row kernel), config 4 as 32
+
+
+def tiles_for(nodes, world):
+    """Column tiles per rank: 8,192-column tiles when the job splits into them evenly."""
+    total = nodes // TILE_COLS
+    if nodes % (2048 * max(total, 1)) != 0 or total < world or total % world != 0 \
+            or total > 64:
+        return 1
+    return total // world
 
 
 def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=False, tiles=None):
@@ -312,15 +323,14 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
         kw.update(events=True, event_cap=EVENT_CAP)
     if dist is not None:
         from gossip_protocol_amd.dist import make_rank_engine
-        if tiles is None:     # 8192-column tiles per rank when the slices are wider (N = 2, 4)
-            tiles = TILES // world if (layout == "columns" and world < TILES and TILES % world == 0
-                                       and nodes % (2048 * TILES) == 0) else 1
+        if tiles is None:     # 8192-column tiles per rank when the slices are wider
+            tiles = tiles_for(nodes, world) if layout == "columns" else 1
         if tiles > 1:
             kw["tiles"] = tiles
         eng = make_rank_engine(nodes, local, **kw)
     else:
         if tiles is None:
-            tiles = TILES if nodes % (2048 * TILES) == 0 else 1
+            tiles = tiles_for(nodes, 1)
         eng = ScaleEngine(nodes, device=local, group=tiles, **kw)
     eng.step(warmup)
     eng.sync()
@@ -366,14 +376,14 @@ def run_full(nodes, steps, warmup, world, local, dist, layout="columns", events=
         m = torch.tensor([el, kern_ms, csr_ms], dtype=torch.float64, device=_dev())
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
         el, kern_ms, csr_ms = (x.item() for x in m)
-    # algorithmic bytes per launch: own row read + write and one sender row per message
+    # algorithmic bytes per tick (all tile launches): own row read + write and one sender row per message
     # (2-byte entries), one 4-byte CSR entry per message; column shards stream their slice
     # (stride columns) of each such row, so the job moves `world` slices; row shards stream
     # whole rows (stride = full width) of their own receivers only
     slices = shards_total if layout == "columns" else 1
-    bytes_per_launch = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
+    bytes_per_tick = ((2.0 * rounds + delivered) * stride * 2.0 + delivered * 4.0) * slices / steps
     return {"el": el, "rounds": rounds, "merges": merges, "kern_ms": kern_ms, "csr_ms": csr_ms,
-            "bytes_per_launch": bytes_per_launch, "xgmi_tick": xgmi_tick, "layout": layout,
+            "bytes_per_tick": bytes_per_tick, "xgmi_tick": xgmi_tick, "layout": layout,
             "events": ev, "tiles": shards_total // (world if dist is not None else 1)}
 
 
@@ -432,7 +442,7 @@ def event_summary(eng, nodes, last_tick, dist, crash):
 
 
 def summarize_full(r, nodes, steps, world):
-    achieved = r["bytes_per_launch"] / (r["kern_ms"] * 1e-3) / 1e9     # summed over ranks
+    achieved = r["bytes_per_tick"] / (r["kern_ms"] * 1e-3) / 1e9     # summed over ranks
     peak = PEAK_HBM_GBS * world
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -459,9 +469,10 @@ def summarize_full(r, nodes, steps, world):
         "xgmi_bytes_per_tick": r["xgmi_tick"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
-                     "kernel_ms": r["kern_ms"], "launches_per_tick": r["tiles"],
+                     "kernel_ms_per_tick": r["kern_ms"], "launches_per_tick": r["tiles"],
+                     "kernel_ms_per_launch": r["kern_ms"] / r["tiles"],
                      ("exchange_csr_ms" if r["layout"] == "rows" else "csr_ms"): r["csr_ms"],
-                     "algorithmic_bytes_per_launch": r["bytes_per_launch"]},
+                     "algorithmic_bytes_per_tick": r["bytes_per_tick"]},
     }
 
 
@@ -486,7 +497,7 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pview", action="store_true", help="skip the config-5 line item")
     ap.add_argument("--pview-nodes", type=int, default=PV_NODES)
-    ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item (N > 1)")
+    ap.add_argument("--no-262k", action="store_true", help="skip the config-4 line item")
     ap.add_argument("--item-budget", type=int, default=420,
                     help="seconds for the secondary line items before the line is printed as is")
     ap.add_argument("--no-events", action="store_true",
@@ -569,13 +580,13 @@ def main(argv=None):
                           False, events=4)
             if r is not None and out is not None and isinstance(out.get("pview"), dict) \
                     and "roofline" in out["pview"]:
-                k0 = out["pview"]["roofline"]["kernel_ms"]
+                k0 = out["pview"]["roofline"]["kernel_ms_per_tick"]
                 r.update(kernel_ms_events_off=k0, kernel_overhead_frac=r["kernel_ms"] / k0 - 1.0)
             return r
         item("pview", _pv_events, "events")
-    if world > 1 and not args.no_262k:
-        # BASELINE config 4: 262,144 nodes full view over the same column shards (its 137 GB
-        # table pair does not fit one GPU next to the runtime, so only N > 1 reports it)
+    if not args.no_262k:
+        # BASELINE config 4: 262,144 nodes full view, 8,192-column tiles: on one GPU 32 tiles
+        # (the table pair is 2 x 128 GiB of the 288 GB HBM), at N > 1 32 / N tiles per rank
         item("full262k", lambda: summarize_full(
             run_full(262144, min(args.steps, 8), 2, world, local, dist), 262144,
             min(args.steps, 8), world))

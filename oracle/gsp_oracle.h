@@ -113,6 +113,10 @@ int32_t gsp_scale_oracle_start_tick(const gsp_scale_oracle *o, int32_t r);
 int64_t gsp_scale_oracle_events(const gsp_scale_oracle *o, int32_t *kind, int32_t *r, int32_t *x,
                                 int64_t cap);
 
+/* OpenMP threads of the scale oracle's step and send phase (0: OpenMP's default; 1: the
+ * single-threaded restatement).  Results do not depend on it. */
+void gsp_oracle_set_threads(int nt);
+
 /* The scale protocol's per-row rules (the reference's, MP1Node.cpp:237-251, 282-301, 339-348),
  * exported so tests can feed them the reference's own rows: one GOSSIP merge, and the
  * TREMOVE scan (returns the gossipable member count). */

@@ -46,6 +46,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <omp.h>
+
 #include "gsp_oracle.h"
 #include "gsp_philox.h"
 
@@ -64,6 +66,28 @@ struct gsp_scale_oracle {
     int32_t *ev_kind, *ev_r, *ev_x; /* events of the last step */
     int64_t nev, evcap;
 };
+
+/* Rows are independent within a phase (every row reads only the previous tick's table), so
+ * the step and the send phase run over contiguous row blocks, one per OpenMP thread; each
+ * block keeps its own messages / events and the blocks are concatenated in row order, so the
+ * result is the sequential one, bit for bit.  gsp_oracle_set_threads(1) gives the
+ * single-threaded restatement (bench.py's CPU baseline). */
+static int g_threads = 0;     /* 0: OpenMP's default */
+void gsp_oracle_set_threads(int nt) { g_threads = nt > 0 ? nt : 0; }
+static int oracle_threads(void) { return g_threads > 0 ? g_threads : omp_get_max_threads(); }
+
+typedef struct { int32_t *a, *b, *c; int64_t n, cap; } triples;
+static void triples_push(triples *v, int32_t a, int32_t b, int32_t c) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 1024;
+        v->a = realloc(v->a, sizeof(int32_t) * v->cap);
+        v->b = realloc(v->b, sizeof(int32_t) * v->cap);
+        v->c = realloc(v->c, sizeof(int32_t) * v->cap);
+    }
+    v->a[v->n] = a; v->b[v->n] = b; v->c[v->n] = c;
+    v->n++;
+}
+static void triples_free(triples *v) { free(v->a); free(v->b); free(v->c); }
 
 uint64_t gsp_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
     uint64_t z = ((uint64_t)kind << 62) | ((uint64_t)(t & 0xFFFFF) << 42) |
@@ -125,42 +149,56 @@ static void send_all(gsp_scale_oracle *o, int tab, int32_t t, gsp_tick_digest *d
     const int32_t n = c->n;
     const int32_t drop = gsp_sched_drop(&c->pol, c->drop_pct, t);
     o->nmsg = 0;
-    int32_t chosen[64];
-    for (int32_t s = 0; s < n; ++s) {
-        if (!alive_at(o, s, t)) continue;
-        const uint8_t *ps = o->pres[tab] + (size_t)s * n;
-        const int32_t *tss = o->ts[tab] + (size_t)s * n;
-        int32_t cnt = o->cnt[s];
-        int32_t keff = c->fanout < cnt ? c->fanout : cnt;
-        int32_t nch = 0;
-        for (int32_t k = 0; k < keff; ++k) {
-            uint32_t u = gsp_philox_u31(GSP_DOMAIN_PEER, c->seed, (uint32_t)t, (uint32_t)s,
-                                        (uint32_t)k, 0);
-            int32_t rk = (int32_t)(u % (uint32_t)(cnt - k));
-            int32_t pos = 0;
-            while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
-            memmove(&chosen[pos + 1], &chosen[pos], sizeof(int32_t) * (nch - pos));
-            chosen[pos] = rk;
-            nch++;
-            int32_t dst = column_of_rank(c, ps, tss, t, rk);
-            if (d) d->sent++;
-            uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, (uint32_t)s,
-                                         (uint32_t)dst, 3u);
-            if ((int32_t)(dr % 100u) < drop) {
-                if (d) d->dropped++;
-                continue;
+    const int nt = oracle_threads();
+    triples *blk = calloc((size_t)nt, sizeof(triples));
+    int64_t sent = 0, dropped = 0;
+#pragma omp parallel num_threads(nt) reduction(+ : sent, dropped)
+    {
+        const int tid = omp_get_thread_num(), nth = omp_get_num_threads();
+        triples *mine = &blk[tid];
+        int32_t chosen[64];
+        for (int32_t s = (int32_t)((int64_t)n * tid / nth); s < (int32_t)((int64_t)n * (tid + 1) / nth); ++s) {
+            if (!alive_at(o, s, t)) continue;
+            const uint8_t *ps = o->pres[tab] + (size_t)s * n;
+            const int32_t *tss = o->ts[tab] + (size_t)s * n;
+            int32_t cnt = o->cnt[s];
+            int32_t keff = c->fanout < cnt ? c->fanout : cnt;
+            int32_t nch = 0;
+            for (int32_t k = 0; k < keff; ++k) {
+                uint32_t u = gsp_philox_u31(GSP_DOMAIN_PEER, c->seed, (uint32_t)t, (uint32_t)s,
+                                            (uint32_t)k, 0);
+                int32_t rk = (int32_t)(u % (uint32_t)(cnt - k));
+                int32_t pos = 0;
+                while (pos < nch && rk >= chosen[pos]) { rk++; pos++; }
+                memmove(&chosen[pos + 1], &chosen[pos], sizeof(int32_t) * (nch - pos));
+                chosen[pos] = rk;
+                nch++;
+                int32_t dst = column_of_rank(c, ps, tss, t, rk);
+                sent++;
+                uint32_t dr = gsp_philox_u31(GSP_DOMAIN_SEND, c->seed, (uint32_t)t, (uint32_t)s,
+                                             (uint32_t)dst, 3u);
+                if ((int32_t)(dr % 100u) < drop) {
+                    dropped++;
+                    continue;
+                }
+                triples_push(mine, s, dst, MSG_GOSSIP);
             }
-            push_msg(o, s, dst, MSG_GOSSIP);
-        }
-        if (c->swim > 0) {      /* the probe target: one more rank-select over the same order */
-            o->ping[s] = -1;
-            if (cnt > 0) {
-                int32_t rk = (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)t,
-                                                      (uint32_t)s, 0, 0x100) % (uint32_t)cnt);
-                o->ping[s] = column_of_rank(c, ps, tss, t, rk);
+            if (c->swim > 0) {  /* the probe target: one more rank-select over the same order */
+                o->ping[s] = -1;
+                if (cnt > 0) {
+                    int32_t rk = (int32_t)(gsp_philox_u31(GSP_DOMAIN_PING, c->seed, (uint32_t)t,
+                                                          (uint32_t)s, 0, 0x100) % (uint32_t)cnt);
+                    o->ping[s] = column_of_rank(c, ps, tss, t, rk);
+                }
             }
         }
     }
+    for (int i = 0; i < nt; ++i) {       /* the blocks in row order: the sequential list */
+        for (int64_t m = 0; m < blk[i].n; ++m) push_msg(o, blk[i].a[m], blk[i].b[m], blk[i].c[m]);
+        triples_free(&blk[i]);
+    }
+    free(blk);
+    if (d) { d->sent += sent; d->dropped += dropped; }
     if (!alive_at(o, 0, t)) return;             /* JOINREPs to the nodes starting at t + 1 */
     for (int32_t j = 1; j < n; ++j) {
         if (o->start_tick[j] != t + 1) continue;
@@ -303,9 +341,16 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
     }
 
     int32_t *cnt_next = malloc(sizeof(int32_t) * n);
+    const int nt = oracle_threads();
+    triples *evb = calloc((size_t)nt, sizeof(triples));
+    gsp_tick_digest *part = calloc((size_t)nt, sizeof(gsp_tick_digest));
+#pragma omp parallel num_threads(nt)
+    {
+    const int tid = omp_get_thread_num(), nth = omp_get_num_threads();
+    gsp_tick_digest *pd = &part[tid];
     uint8_t *Pj = malloc((size_t)n), *P0 = malloc((size_t)n);
     int32_t ranks[16];
-    for (int32_t r = 0; r < n; ++r) {
+    for (int32_t r = (int32_t)((int64_t)n * tid / nth); r < (int32_t)((int64_t)n * (tid + 1) / nth); ++r) {
         const size_t row = (size_t)r * n;
         uint8_t *P = o->pres[next] + row;
         int32_t *H = o->hb[next] + row, *S = o->ts[next] + row;
@@ -313,14 +358,14 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
         memcpy(H, o->hb[prev] + row, sizeof(int32_t) * n);
         memcpy(S, o->ts[prev] + row, sizeof(int32_t) * n);
         if (!alive_at(o, r, t)) { cnt_next[r] = o->cnt[r]; continue; }
-        d->node_rounds++;
+        pd->node_rounds++;
         memcpy(P0, P, n);
         for (int32_t j = deg[r]; j < deg[r + 1]; ++j) {
             const int32_t m = bucket[j], s = o->msrc[m];
             const size_t srow = (size_t)s * n;
             const uint8_t *Ps = o->pres[prev] + srow;
             const int32_t *Hs = o->hb[prev] + srow, *Ss = o->ts[prev] + srow;
-            d->delivered++;
+            pd->delivered++;
             if (o->mtype[m] == MSG_JOINREP) {
                 /* the bounded introducer list: the chosen ranks among node 0's gossipable
                  * members of tick t - 1 */
@@ -330,14 +375,14 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
                     const int32_t x = column_of_rank(c, Ps, Ss, t - 1, ranks[i]);
                     if (x >= 0) Pj[x] = 1;
                 }
-                d->merges += 1 + b;
-                gsp_scale_oracle_merge_msg(n, t, T, 0, r, P, H, S, s, Pj, Hs, Ss, &d->joins,
-                                           &d->event_hash);
+                pd->merges += 1 + b;
+                gsp_scale_oracle_merge_msg(n, t, T, 0, r, P, H, S, s, Pj, Hs, Ss, &pd->joins,
+                                           &pd->event_hash);
             } else {
-                d->merges += 1 + o->cnt[s];
+                pd->merges += 1 + o->cnt[s];
                 /* the payload: s's members gossipable when s sent it (tick t - 1) */
                 gsp_scale_oracle_merge_msg(n, t, T, c->tfail, r, P, H, S, s, Ps, Hs, Ss,
-                                           &d->joins, &d->event_hash);
+                                           &pd->joins, &pd->event_hash);
             }
         }
         if (c->swim > 0 && o->ping[r] >= 0) {   /* resolve the probe sent at t - 1 */
@@ -351,14 +396,27 @@ int gsp_scale_oracle_step(gsp_scale_oracle *o, gsp_tick_digest *d) {
         }
         o->own_hb[r] += 1;
         for (int32_t x = 0; x < n; ++x)         /* the row's join events, then its removes */
-            if (P[x] && !P0[x]) push_event(o, 1, r, x);
+            if (P[x] && !P0[x]) triples_push(&evb[tid], 1, r, x);
         for (int32_t x = 0; x < n; ++x)
-            if (P[x] && t - S[x] >= T) push_event(o, 2, r, x);
-        cnt_next[r] = gsp_scale_oracle_remove_scan(n, t, T, c->tfail, r, P, H, S, &d->removes,
-                                                   &d->event_hash);
+            if (P[x] && t - S[x] >= T) triples_push(&evb[tid], 2, r, x);
+        cnt_next[r] = gsp_scale_oracle_remove_scan(n, t, T, c->tfail, r, P, H, S, &pd->removes,
+                                                   &pd->event_hash);
     }
     free(Pj);
     free(P0);
+    }
+    for (int i = 0; i < nt; ++i) {       /* digest sums; events in row order */
+        d->node_rounds += part[i].node_rounds;
+        d->delivered += part[i].delivered;
+        d->merges += part[i].merges;
+        d->joins += part[i].joins;
+        d->removes += part[i].removes;
+        d->event_hash += part[i].event_hash;
+        for (int64_t e = 0; e < evb[i].n; ++e) push_event(o, evb[i].a[e], evb[i].b[e], evb[i].c[e]);
+        triples_free(&evb[i]);
+    }
+    free(evb);
+    free(part);
     memcpy(o->cnt, cnt_next, sizeof(int32_t) * n);
     free(cnt_next); free(deg); free(fill); free(bucket);
     o->cur = next;

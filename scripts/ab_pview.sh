@@ -10,7 +10,7 @@ for v in "$@"; do
     if [ "$v" = base ]; then VAR=""; else VAR="$v"; fi
     GSP_LIB_VARIANT=$VAR timeout -k 10 150 python3 -u scripts/bench_pview.py --steps 10 --warmup 5 --no-cpu-baseline > "$OUT/$v.log" 2>&1
     rc=$?
-    echo "$v rc=$rc $(tail -1 "$OUT/$v.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("kernel_ms=%.3f ms_per_step=%.3f" % (d["roofline"]["kernel_ms"], d["ms_per_step"]))' 2>/dev/null)"
+    echo "$v rc=$rc $(tail -1 "$OUT/$v.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("kernel_ms=%.3f ms_per_step=%.3f" % (d["roofline"]["kernel_ms_per_tick"], d["ms_per_step"]))' 2>/dev/null)"
     [ $rc -ne 0 ] && exit $rc
 done
 echo done

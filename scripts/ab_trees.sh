@@ -18,6 +18,6 @@ for i in $(seq "$REPS"); do
             (cd "$dir" && timeout -k 10 150 python3 -u scripts/bench_pview.py --steps 10 --warmup 5 \
                 --no-cpu-baseline) > "$OUT/$side.$i.log" 2>&1
         fi
-        echo "$side $i $(tail -1 "$OUT/$side.$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("kernel_ms=%.3f" % d["roofline"]["kernel_ms"])')"
+        echo "$side $i $(tail -1 "$OUT/$side.$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("kernel_ms=%.3f" % d["roofline"]["kernel_ms_per_tick"])')"
     done
 done

@@ -124,6 +124,7 @@ def load_oracle():
         L.gsp_scale_oracle_messages.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_int64]
         L.gsp_scale_oracle_messages.restype = ctypes.c_int64
+        L.gsp_oracle_set_threads.argtypes = [ctypes.c_int]
         L.gsp_event_mix.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
         L.gsp_event_mix.restype = ctypes.c_uint64
         L.gsp_pview_oracle_create.argtypes = [ctypes.POINTER(PviewCfg)]

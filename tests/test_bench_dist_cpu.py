@@ -106,16 +106,16 @@ def test_bench_two_ranks_gloo():
     assert d["n_gpus"] == 2 and d["steps"] == N_STEPS and d["warmup"] == N_WARM
     assert d["config"]["parallelism"] == "columns2"
     rf = d["roofline"]
-    assert rf["kernel_ms"] == 3.0                     # slowest rank
+    assert rf["kernel_ms_per_tick"] == 3.0                     # slowest rank
     assert rf["peak"] == 16000.0
     # job bytes per launch: (2 rows + 2 rows delivered) * stride(512) * 2 B + CSR, x 2 slices
-    assert rf["algorithmic_bytes_per_launch"] == ((2 * 1024 + 2 * 1024) * 512 * 2 + 2 * 1024 * 4) * 2
+    assert rf["algorithmic_bytes_per_tick"] == ((2 * 1024 + 2 * 1024) * 512 * 2 + 2 * 1024 * 4) * 2
     assert abs(d["value"] - 1024 * N_STEPS / (d["ms_per_step"] * N_STEPS / 1e3)) < 1e-6 * d["value"]
     assert d["xgmi_bytes_per_tick"] == 3000.0         # sum over ranks
     pv = d["pview"]
     assert pv["config"]["parallelism"] == "rows2"
     assert pv["xgmi_bytes_per_tick"] == 3000.0
-    assert pv["roofline"]["kernel_ms"] == 3.0
+    assert pv["roofline"]["kernel_ms_per_tick"] == 3.0
     assert abs(pv["value"] - 4096 * min(N_STEPS, 30) / (pv["ms_per_step"] * min(N_STEPS, 30) / 1e3)) \
         < 1e-6 * pv["value"]
     f = d["full262k"]
@@ -124,7 +124,7 @@ def test_bench_two_ranks_gloo():
     c3 = fr["config3"]
     assert c3["config"]["parallelism"] == "rows2"
     # row shards: whole rows (stride = n) of their own receivers, no slice factor
-    assert c3["roofline"]["algorithmic_bytes_per_launch"] == \
+    assert c3["roofline"]["algorithmic_bytes_per_tick"] == \
         (2 * 512 + 2 * 512) * 2 * 1024 * 2 + 2 * 512 * 2 * 4
     assert abs(c3["value"] - 1024 * min(N_STEPS, 8) / (c3["ms_per_step"] * min(N_STEPS, 8) / 1e3)) \
         < 1e-6 * c3["value"]

@@ -202,6 +202,68 @@ def test_rccl_rank_path_one_rank(tfail, swim):
         _compare_state(eng, orc, n, range(0, n, 37))
 
 
+# The launch form bench.py's headline runs (ScaleEngine(65536, group=8): 8 in-process column
+# tiles sharing one CSR, one count table, one pick resolve over every tile's bitmap and one
+# finalize; DESIGN.md "Column tiles"), against the oracle at n where it runs in seconds:
+# n = 16,384 gives 2,048-column tiles; n = 12,000 a ragged tile 5 (columns 10,240..11,999)
+# and two empty tiles.  The per-entry rules are MP1Node.cpp:234-256 (merge) and :335-348 (ops).
+RANDOM8 = dict(fanout=3, drop_pct=10, fail_mode=FAIL_RANDOM, fail_tick=6, fail_ppm=20000,
+               seed=21, tremove=8)
+COLUMNS8 = [
+    # id, n, engine / oracle keywords, policy, events, ticks
+    ("plain", 16384, RANDOM8, None, False, 16),
+    ("ragged", 12000, dict(fanout=4, drop_pct=0, fail_mode=FAIL_BLOCK, fail_tick=5,
+                           fail_ppm=50000, seed=5, tremove=7), None, False, 15),
+    ("tfail_swim", 16384, dict(RANDOM8, drop_pct=20, seed=33, tremove=9, tfail=4, swim=2), None,
+     False, 15),
+    ("policy_events", 16384, dict(RANDOM8, seed=44), dict(
+        drop_window=(3, 9), step_rate=0.005, intro_list=8, fail_events=[(9, 3, 0), (11, 2, 20000)]),
+     True, 15),
+]
+
+
+@pytest.mark.parametrize("case", COLUMNS8, ids=lambda c: c[0])
+def test_columns8_matches_oracle(case):
+    """8 column tiles in one process (the headline form) = the oracle: every digest, every
+    tick's event multiset (policy case), messages and sampled rows along the run, then every
+    61st row in full."""
+    from gossip_protocol_amd import _lib
+    from gossip_protocol_amd.scale import make_policy
+    from tests.oracle_binding import make_policy as oracle_policy
+    _, n, kw, pol, events, ticks = case
+    orc = ScaleOracle(n, policy=oracle_policy(**pol) if pol else None, **kw)
+    rng = np.random.default_rng(n)
+    with ScaleEngine(n, max_ticks=ticks, group=8, policy=make_policy(**pol) if pol else None,
+                     events=events, **kw) as eng:
+        assert eng.layout() == (8, 0, 2048)
+        src, dst = orc.messages()
+        m = eng.messages()
+        assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+            sorted(zip(src.tolist(), dst.tolist()))
+        if events:
+            eng.drain_events()
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d\n got %s\nwant %s" % (t, eng.digest(t), want)
+            if events:
+                rec, lost = eng.drain_events()
+                k, tk, r, x = _lib.split_events(rec)
+                ok, orr, ox = orc.events()
+                assert lost == 0 and np.all(tk == t)
+                assert sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                    sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), "events tick %d" % t
+            if t % 5 == 0 or t == kw["fail_tick"] + 1:
+                src, dst = orc.messages()
+                m = eng.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+                rows = sorted(set(rng.integers(0, n, 16).tolist()) | {0, 2047, 2048, n - 1})
+                _compare_state(eng, orc, n, rows)
+        _compare_state(eng, orc, n, range(0, n, 61))
+    orc.close()
+
+
 def test_columns_equal_fused_full_size():
     """Config-3 size: 4 column shards (in-process exchange) give the one-GPU results."""
     n, ticks = 65536, 14
@@ -220,6 +282,42 @@ def test_columns_equal_fused_full_size():
             assert np.array_equal(b.row(r), row), r
         assert np.array_equal(b.messages(), ma)
     assert da == db
+
+
+def test_columns8_equal_fused_full_size_with_events():
+    """The headline workload itself (config 3: 65,536 nodes, fanout 3, 1 % random crash; here
+    at t = 2 so that the removals start inside the run) as bench.py launches it -- 8 column
+    tiles -- against the fused one-GPU kernel: every tick's digest, every tick's drained event
+    records (sorted 64-bit records, tick field included), the messages and sampled rows."""
+    n, ticks = 65536, 30
+    kw = dict(fanout=3, fail_mode=FAIL_RANDOM, fail_tick=2, fail_ppm=10000, seed=0x5EED,
+              max_ticks=ticks, events=True, event_cap=1 << 26)
+    rows = (0, 8191, 8192, 40000, n - 1)
+    ref = {}
+    with ScaleEngine(n, **kw) as a:
+        a.drain_events()
+        for t in range(1, ticks + 1):
+            a.step(1)
+            rec, lost = a.drain_events()
+            assert lost == 0
+            ref[t] = (a.digest(t), np.sort(rec))
+        ra = {r: a.row(r) for r in rows}
+        ma = a.messages()
+    removes = 0
+    with ScaleEngine(n, group=8, **kw) as b:
+        assert b.layout() == (8, 0, 8192)
+        b.drain_events()
+        for t in range(1, ticks + 1):
+            b.step(1)
+            rec, lost = b.drain_events()
+            assert lost == 0
+            assert b.digest(t) == ref[t][0], t
+            assert np.array_equal(np.sort(rec), ref[t][1]), "event records of tick %d" % t
+            removes += b.digest(t)["removes"]
+        for r, row in ra.items():
+            assert np.array_equal(b.row(r), row), r
+        assert np.array_equal(b.messages(), ma)
+    assert removes > 1000000          # the crash wave (655 nodes) is inside the run
 
 
 def test_rows_equal_fused_full_size():
@@ -369,3 +467,46 @@ def test_rccl_rank_path_tiled(tiles, variant):
             sorted(zip(src.tolist(), dst.tolist()))
         _compare_state(eng, orc, n, range(0, n, 131))
     orc.close()
+
+
+def test_config4_one_gpu_32_tiles_properties():
+    """BASELINE config 4 (262,144 nodes, full view) on ONE GPU: 32 in-process column tiles of
+    8,192 columns (the tile width config 3 runs fastest at); the table pair is 2 x 128 GiB of
+    the MI355X's HBM.  Size-independent properties, as test_scale_full_size_properties:
+    conservation of messages, node-rounds = alive nodes, and three rows of tick t + 1
+    recomputed on the host from the tick-t rows and the message list with the reference's
+    per-entry rules (MP1Node.cpp:234-256 merge, :335-348 TREMOVE)."""
+    n = 262144
+    with ScaleEngine(n, fanout=3, drop_pct=0, fail_mode=FAIL_RANDOM, fail_tick=3,
+                     fail_ppm=10000, seed=0x5EED, max_ticks=8, group=32) as eng:
+        assert eng.layout() == (32, 0, 8192)
+        eng.step(5)
+        d3, d4, d5 = eng.digest(3), eng.digest(4), eng.digest(5)
+        alive = d5["node_rounds"]
+        assert d3["node_rounds"] == n and d4["node_rounds"] == alive
+        assert 0.985 * n < alive < 0.995 * n          # nodes crash at the end of tick 3
+        assert d5["delivered"] <= d4["sent"] - d4["dropped"]
+        assert d5["merges"] >= d5["delivered"] and d5["sent"] == 3 * alive
+        msgs = eng.messages()           # sent at tick 5, delivered at 6
+        from gossip_protocol_amd import _lib
+        crash = _lib.fail_schedule(n, 0x5EED, FAIL_RANDOM, 3, 10000)
+        targets = [r for r in (7, 8, 131071, 131072, n - 2, n - 3) if crash[r] > 6][::2][:3]
+        dst = msgs.reshape(-1)
+        src = np.repeat(np.arange(n), 3)
+        senders = {r: sorted(src[dst == r].tolist()) for r in targets}
+        need = set(targets) | {s for v in senders.values() for s in v}
+        rows_prev = {r: eng.row(r).astype(np.uint32) for r in need}
+        eng.step(1)
+        t5, tr = 6 & 31, 20
+        for r in targets:
+            e = rows_prev[r].copy()
+            for s in senders[r]:
+                v = rows_prev[s]
+                he, hv = e >> 5, v >> 5
+                upd = np.where(hv > he, (v & 0xFFE0) | t5, e)
+                add = np.where((v != 0) & (((t5 - v) & 31) < tr), v, 0)
+                e = np.where(e != 0, upd, add)
+                e[s] = (((e[s] >> 5) + 1) << 5) | t5
+            e[r] = 0
+            e = np.where((e != 0) & (((t5 - e) & 31) >= tr), 0, e)
+            assert np.array_equal(e.astype(np.uint16), eng.row(r)), "row %d" % r

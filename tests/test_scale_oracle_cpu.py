@@ -104,3 +104,31 @@ def test_swim_detects_crashes_before_tremove():
     assert detected > 0                             # probes removed crashed members by tick 20
     o.close()
     plain.close()
+
+
+def test_threaded_oracle_equals_single_threaded():
+    """The oracle's step and send phase run over row blocks on OpenMP threads, concatenated in
+    row order: every digest, message list, event list and row equals the one-thread run."""
+    from tests.oracle_binding import load_oracle, make_policy
+    L = load_oracle()
+    kw = dict(fanout=3, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=40000, seed=21, tremove=8,
+              swim=2, tfail=4, policy=make_policy(step_rate=0.05, intro_list=3, drop_window=(2, 9)))
+    runs = []
+    try:
+        for threads in (1, 5):
+            L.gsp_oracle_set_threads(threads)
+            o = ScaleOracle(203, **kw)
+            trace = []
+            for _ in range(18):
+                d = o.step()
+                src, dst = o.messages()
+                k, r, x = o.events()
+                trace.append((d, src.tolist(), dst.tolist(), k.tolist(), r.tolist(), x.tolist(),
+                              o.joinreps().tolist()))
+            rows = [tuple(a.tolist() for a in o.row(r)) for r in range(203)]
+            runs.append((trace, rows))
+            o.close()
+    finally:
+        L.gsp_oracle_set_threads(0)
+    assert runs[0] == runs[1]
+    assert sum(len(t[3]) for t in runs[0][0]) > 0
