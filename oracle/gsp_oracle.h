@@ -183,5 +183,14 @@ int32_t gsp_pview_oracle_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r,
                                   const int32_t *sv_hb, const int32_t *sv_ts,
                                   const int32_t *sv_len, int32_t *out_id, int32_t *out_hb,
                                   int32_t *out_ts, gsp_pview_digest *d);
+/* The partial view's per-entry rules on their own (the ones gsp_pview_oracle_step folds
+ * with): one GOSSIP merged into a view (ids ascending; returns the new length, -1 past cap),
+ * and the TREMOVE scan (returns the new length). */
+int32_t gsp_pview_oracle_merge_msg(int32_t t, int32_t T, int32_t r, int32_t *id, int32_t *hb,
+                                   int32_t *ts, int32_t len, int32_t cap, int32_t s,
+                                   const int32_t *p_id, const int32_t *p_hb, const int32_t *p_ts,
+                                   int32_t plen, int64_t *joins);
+int32_t gsp_pview_oracle_remove_scan(int32_t t, int32_t T, int32_t *id, int32_t *hb, int32_t *ts,
+                                     int32_t len, int64_t *removes);
 
 #endif

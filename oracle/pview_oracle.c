@@ -241,6 +241,27 @@ static int cmp_id(const void *a, const void *b) {
     return (x->id > y->id) - (x->id < y->id);
 }
 
+/* The reference's per-entry rules for member id x of receiver r at tick t, one message from
+ * sender s whose payload holds v for x (NULL: no entry): the fold of pv_row_step and the
+ * per-message merge exported below (gsp_pview_oracle_merge_msg) are both made of this. */
+static inline void pv_rule(int32_t t, int32_t T, int32_t r, int32_t x, int32_t s, const pv_ent *v,
+                           int *present, pv_ent *cur) {
+    if (x == s) {                                   /* MP1Node.cpp:237-243 */
+        if (*present) { cur->hb += 1; cur->ts = t; }
+        else { *present = 1; cur->hb = 1; cur->ts = t; }
+        return;
+    }
+    if (!v) return;
+    if (*present) {                                 /* MP1Node.cpp:247-251 */
+        if (v->hb > cur->hb) { cur->hb = v->hb; cur->ts = t; }
+    } else if (x != r && t - v->ts < T) {           /* MP1Node.cpp:282-301 */
+        *present = 1; cur->hb = v->hb; cur->ts = v->ts;
+    }
+}
+
+/* nodeLoopOps' TREMOVE predicate (MP1Node.cpp:340) */
+static inline int pv_expired(int32_t t, int32_t T, int32_t ts) { return t - ts >= T; }
+
 /* One alive receiver's tick t: merge the payloads sv[j] (sorted by id, already cut to what
  * the message carries) of the k senders b[j] (ascending) into its own view, resolve the SWIM
  * probe (probe_x >= 0), TREMOVE scan, eviction to V.  Writes the new view to out (sorted by
@@ -269,28 +290,15 @@ static int32_t pv_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r, const p
         const pv_ent *e0 = find_id(own, own_len, x);
         int present = e0 != NULL;
         pv_ent cur = e0 ? *e0 : (pv_ent){x, 0, 0};
-        for (int32_t j = 0; j < k; ++j) {
-            const int32_t s = b[j];
-            if (x == s) {                                   /* MP1Node.cpp:237-243 */
-                if (present) { cur.hb += 1; cur.ts = t; }
-                else { present = 1; cur.hb = 1; cur.ts = t; }
-                continue;
-            }
-            const pv_ent *v = find_id(sv[j], slen[j], x);
-            if (!v) continue;
-            if (present) {                                  /* MP1Node.cpp:247-251 */
-                if (v->hb > cur.hb) { cur.hb = v->hb; cur.ts = t; }
-            } else if (x != r && t - v->ts < T) {           /* MP1Node.cpp:282-301 */
-                present = 1; cur.hb = v->hb; cur.ts = v->ts;
-            }
-        }
+        for (int32_t j = 0; j < k; ++j)
+            pv_rule(t, T, r, x, b[j], b[j] == x ? NULL : find_id(sv[j], slen[j], x), &present, &cur);
         if (!present) continue;
         if (x == probe_x) cur.ts = probe_ok ? t : t - T;   /* SWIM: the probe's answer */
         if (!e0) {
             d->joins++; d->event_hash += gsp_pv_event_mix(1, t, r, x);
             push_event(sk, 1, r, x);
         }
-        if (t - cur.ts >= T) {                              /* MP1Node.cpp:340 */
+        if (pv_expired(t, T, cur.ts)) {                     /* MP1Node.cpp:340 */
             d->removes++; d->event_hash += gsp_pv_event_mix(2, t, r, x);
             push_event(sk, 2, r, x);
             continue;
@@ -360,6 +368,56 @@ int32_t gsp_pview_oracle_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r,
     for (int32_t i = 0; i < m; ++i) { out_id[i] = out[i].id; out_hb[i] = out[i].hb; out_ts[i] = out[i].ts; }
     free(order); free(own); free(views); free(sv); free(b); free(slen); free(ids); free(res);
     free(out); free(kk);
+    return m;
+}
+
+/* ---- the per-entry rules on their own, exported (tests/test_pview_rules_vs_reference.py
+ * feeds them the reference's own rows in the reference's own message order) ---- */
+
+/* Receiver r's view (ids ascending; id / hb / ts, len entries, room for cap) merges ONE
+ * GOSSIP sent by s whose payload is p (ids ascending, plen entries) at tick t: pv_rule for
+ * every id of the view, of the payload and s itself.  New members count into *joins.
+ * Returns the new length, or -1 when it would exceed cap (no eviction here). */
+int32_t gsp_pview_oracle_merge_msg(int32_t t, int32_t T, int32_t r, int32_t *id, int32_t *hb,
+                                   int32_t *ts, int32_t len, int32_t cap, int32_t s,
+                                   const int32_t *p_id, const int32_t *p_hb, const int32_t *p_ts,
+                                   int32_t plen, int64_t *joins) {
+    pv_ent *own = malloc(sizeof(pv_ent) * (size_t)(len + 1));
+    pv_ent *pay = malloc(sizeof(pv_ent) * (size_t)(plen + 1));
+    pv_ent *res = malloc(sizeof(pv_ent) * (size_t)(len + plen + 1));
+    int32_t *ids = malloc(sizeof(int32_t) * (size_t)(len + plen + 1));
+    int32_t nid = 0, nres = 0;
+    for (int32_t i = 0; i < len; ++i) { own[i] = (pv_ent){id[i], hb[i], ts[i]}; ids[nid++] = id[i]; }
+    for (int32_t i = 0; i < plen; ++i) { pay[i] = (pv_ent){p_id[i], p_hb[i], p_ts[i]}; ids[nid++] = p_id[i]; }
+    ids[nid++] = s;
+    qsort(ids, nid, sizeof(int32_t), cmp_i32);
+    for (int32_t i = 0; i < nid; ++i) {
+        if (i && ids[i] == ids[i - 1]) continue;
+        const int32_t x = ids[i];
+        const pv_ent *e0 = find_id(own, len, x);
+        int present = e0 != NULL;
+        pv_ent cur = e0 ? *e0 : (pv_ent){x, 0, 0};
+        pv_rule(t, T, r, x, s, x == s ? NULL : find_id(pay, plen, x), &present, &cur);
+        if (!present) continue;
+        if (!e0 && joins) (*joins)++;
+        res[nres++] = cur;
+    }
+    if (nres <= cap)
+        for (int32_t i = 0; i < nres; ++i) { id[i] = res[i].id; hb[i] = res[i].hb; ts[i] = res[i].ts; }
+    free(own); free(pay); free(res); free(ids);
+    return nres <= cap ? nres : -1;
+}
+
+/* nodeLoopOps' TREMOVE scan of a view at tick t (pv_expired, MP1Node.cpp:339-348): removes
+ * in place, keeps id order, counts into *removes; returns the new length. */
+int32_t gsp_pview_oracle_remove_scan(int32_t t, int32_t T, int32_t *id, int32_t *hb, int32_t *ts,
+                                     int32_t len, int64_t *removes) {
+    int32_t m = 0;
+    for (int32_t i = 0; i < len; ++i) {
+        if (pv_expired(t, T, ts[i])) { if (removes) (*removes)++; continue; }
+        id[m] = id[i]; hb[m] = hb[i]; ts[m] = ts[i];
+        m++;
+    }
     return m;
 }
 
