@@ -23,7 +23,7 @@ OBJS     := $(patsubst $(CSRC)/%.hip,build/%.hip.o,$(KERNELS)) \
             $(patsubst $(CSRC)/%.cpp,build/%.cpp.o,$(HOSTSRC))
 HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard include/gossip/*.h) $(wildcard include/gossip/*.hpp)
 
-.PHONY: all lib app oracle clean lib-variant
+.PHONY: all lib app oracle clean lib-variant pv-variant
 all: lib app oracle
 
 lib: $(LIB)
@@ -32,11 +32,15 @@ app: $(APP)
 build:
 	mkdir -p build
 
-build/%.hip.o: $(CSRC)/%.hip $(HDRS) | build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+# header dependencies from the compiler (-MMD): an object rebuilds when a header it includes
+# changes, not on every header edit (pview_kernels.hip alone takes minutes)
+build/%.hip.o: $(CSRC)/%.hip | build
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
 
-build/%.cpp.o: $(CSRC)/%.cpp $(HDRS) | build
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+build/%.cpp.o: $(CSRC)/%.cpp | build
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+-include $(wildcard build/*.d)
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $(OBJS) $(LDFLAGS)
@@ -56,6 +60,14 @@ lib-variant: $(KERNELS) $(HOSTSRC) $(HDRS)
 	for f in $(KERNELS) $(HOSTSRC); do \
 	  $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o build/v-$(TAG)/$$(basename $$f).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -o $(PKG)/libgossip_amd.$(TAG).so build/v-$(TAG)/*.o $(LDFLAGS)
+
+# partial-view kernel A/B variant, rebuilding only pview_kernels.hip (the other objects come
+# from build/): make pv-variant TAG=x VFLAGS=-DGSP_...  ->  $(PKG)/libgossip_amd.x.so
+pv-variant: $(OBJS)
+	mkdir -p build/v-$(TAG)
+	$(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $(CSRC)/pview_kernels.hip -o build/v-$(TAG)/pview_kernels.hip.o
+	$(HIPCC) --offload-arch=$(ARCH) -o $(PKG)/libgossip_amd.$(TAG).so build/v-$(TAG)/pview_kernels.hip.o \
+	    $(filter-out build/pview_kernels.hip.o,$(OBJS)) $(LDFLAGS)
 
 clean:
 	rm -rf build $(LIB) $(PKG)/libgossip_amd.*.so $(PKG)/bin

@@ -7,8 +7,10 @@
 //   MAX_NNB          n
 //   SINGLE_FAILURE   1: one Philox-chosen node crashes at t = 100 (Application.cpp:180-187),
 //                    0: n/2 contiguous nodes from (Philox % n)/2 at t = 100 (:188-196)
-//   DROP_MSG         1: drop_pct = (int)(MSG_DROP_PROB * 100) (EmulNet.cpp:91) in the window
-//                    [50, 300) (Application.cpp:177, 198); 0: no drops
+//   DROP_MSG         1: drop_pct = (int)(MSG_DROP_PROB * 100) (EmulNet.cpp:91) for the sends of
+//                    ticks [51, 301): fail() sets dropmsg at the END of t = 50, after that
+//                    tick's mp1Run, and clears it at the end of t = 300 (Application.cpp:99-104,
+//                    177, 198) -- the same end-of-tick rule as the crash events; 0: no drops
 //   (fixed)          STEP_RATE 0.25 (Params.cpp:30), 700 ticks (Application.h:27), TREMOVE 20
 // Any further lines are optional "KEY: value..." pairs that the reference's fscanf never
 // reaches (they follow the fourth key):
@@ -67,8 +69,8 @@ int read_conf(const char *path, ConfAll &c) {
     c.first = gsp_fail_event{100, single ? GSP_FAIL_SINGLE : GSP_FAIL_HALF, 0};
     if (drop) {
         c.drop_pct = int32_t(prob * 100);             // EmulNet.cpp:91
-        c.pol.drop_from = 50;
-        c.pol.drop_until = 300;
+        c.pol.drop_from = 51;                          // set at the end of t = 50
+        c.pol.drop_until = 301;                        // cleared at the end of t = 300
     }
     c.pol.step_rate = 0.25;                            // Params.cpp:30
     bool first_fail = true;

@@ -25,11 +25,18 @@ hipError_t EvRing::drain(uint64_t *out, int64_t cap, int64_t *n, int64_t *lost) 
         const int64_t got = int64_t(c[size_t(s) * kEvCounterStride]);
         const int64_t have = std::min(got, stripe_cap);
         *lost += got - have;
-        if (out && *n < cap && have > 0)
-            if (hipError_t e = hipMemcpy(out + *n, buf.p + int64_t(s) * stripe_cap,
-                                         size_t(std::min(have, cap - *n)) * 8, hipMemcpyDeviceToHost))
+        if (!out) {                        // counting only: the ring is kept
+            *n += have;
+            continue;
+        }
+        // the records past cap are dropped with the ring: counted as lost, never in *n
+        const int64_t take = std::max<int64_t>(0, std::min(have, cap - *n));
+        if (take > 0)
+            if (hipError_t e = hipMemcpy(out + *n, buf.p + int64_t(s) * stripe_cap, size_t(take) * 8,
+                                         hipMemcpyDeviceToHost))
                 return e;
-        *n += have;
+        *n += take;
+        *lost += have - take;
     }
     if (out) return hipMemset(count.p, 0, size_t(kEvStripes) * kEvCounterStride * 8);
     return hipSuccess;

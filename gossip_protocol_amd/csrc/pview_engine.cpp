@@ -72,14 +72,16 @@ struct gsp_pview {
     int64_t pair_cap = 0, msg_cap = 0;
     int32_t tick = 0;
     bool timing = true;
-    int32_t waves = 8;           // tick-kernel variant (GSP_PV_WAVES=7|8)
-    int32_t split = 9;           // GSP_PV_SPLIT bits (pview_kernels.hip): 1 rows merging <= 3
-                                 // messages as 128-lane rows, 8 also k = 4, 5 in their own kernels
-                                 // (2 small rows first, 32 k = 0 rows alone; 0: one kernel)
-    bool split_sync = true;      // exact split grids from the counts read back, one stream sync
-                                 // per tick (GSP_PV_SPLITSYNC=0: grids of every row, the rows past a
-                                 // bucket range return at once; A/B 6.14 vs 5.95 ms per tick)
+    int32_t split = 1;           // GSP_PV_SPLIT=0: every row in the one 256-lane kernel; else
+                                 // rows bucketed by k into four kernels (pview_kernels.hip)
+    bool split_sync = false;     // GSP_PV_SPLITSYNC=1: exact split grids from the counts read
+                                 // back, one stream sync per tick; default: persistent grids, no
+                                 // host wait (gsp_pview_step queues its ticks back to back)
+    int32_t cus = 0;             // compute units (overflow kernel grid)
+    int32_t test_grid_cap = 0;   // GSP_TEST_PV_GRID_CAP (tests: force the overflow kernel)
     int32_t *h_kcount = nullptr; // pinned [8] for split_sync
+    int32_t *h_kseen = nullptr;  // pinned [local][8]: each shard's bucket sizes, copied back
+                                 // asynchronously every tick (they size the next tick's grids)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
@@ -87,7 +89,7 @@ struct gsp_pview {
     std::vector<int32_t> h_fail, h_start;
     bool joins = false;          // a join schedule is set (some node starts after tick 0)
     gsp::JoinPlan plan;
-    int32_t *h_cnt = nullptr;    // pinned [G][2G]: pair counts then record counts per shard
+    int32_t *h_cnt = nullptr;    // pinned [G][2G + 1]: pair counts, record counts, capacity flag
     int32_t *h_recv = nullptr;   // pinned [local][G]: records each local shard receives
     struct Timed { hipEvent_t a, b, c; };
     std::vector<Timed> pending;
@@ -138,14 +140,16 @@ struct gsp_pview {
         a.rowdig = sh.rowdig.p;
         a.deg = sh.deg.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
-        a.err = sh.err.p;
+        a.err = local[0].err.p;        // one flag for every shard held here
         a.max_segment = max_segment;
         a.kcount = sort_rows ? sh.kcount.p : nullptr;
         a.order = sort_rows ? sh.order.p : nullptr;
         a.prof = sh.prof.p;
-        a.waves = waves;
         a.split = split;
         a.kcount_host = h_kcount;
+        a.kcount_seen = h_kseen ? h_kseen + 8 * (&sh - local.data()) : nullptr;
+        a.cus = cus;
+        a.test_grid_cap = test_grid_cap;
         a.ev = sh.ev.args();
         return a;
     }
@@ -165,7 +169,7 @@ struct gsp_pview {
         a.rc_slot = sh.rc_slot.p;
         a.kcount = sort_rows ? sh.kcount.p : nullptr;
         a.order = sort_rows ? sh.order.p : nullptr;
-        a.err = sh.err.p;
+        a.err = local[0].err.p;
         return a;
     }
 
@@ -271,13 +275,16 @@ int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
     std::vector<gsp::RowxShard> v;
     for (PvShard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p, sh.table[t_sent & 1].p,
-                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p, &sh.x});
+                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p,
+                                   s->local[0].err.p, &sh.x});
     return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
 }
 
-// The capacity flags as last mirrored to the host: a receiver sent more than max_segment
-// messages at tick t sets its shard's flag to t, and the tick kernels of t and every later
-// tick run no row, so the job's state stays that of tick t - 1.
+// The capacity flag as last mirrored to the host: a receiver sent more than max_segment
+// messages at tick t sets the flag to t, and the tick kernels of t and every later tick run no
+// row, so the job's state stays that of tick t - 1.  Every shard held by this engine reads one
+// flag (shard 0's), so an in-process group stops as a whole; ranks of a communicator
+// exchange their flags with the row-exchange counts and stop at the same tick.
 int pview_mirrored_err(gsp_pview *s) {
     for (size_t i = 0; i < s->local.size(); ++i)
         GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
@@ -373,12 +380,17 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->shards = shards;
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
-    if (const char *w = std::getenv("GSP_PV_WAVES")) s->waves = std::atoi(w) == 7 ? 7 : 8;
     if (const char *sp = std::getenv("GSP_PV_SPLIT")) s->split = std::atoi(sp);
     if (const char *ss = std::getenv("GSP_PV_SPLITSYNC")) s->split_sync = std::atoi(ss) != 0;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
+    if (const char *gc = std::getenv("GSP_TEST_PV_GRID_CAP")) s->test_grid_cap = std::max(0, std::atoi(gc));
     if (s->split_sync && s->split && s->sort_rows)
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
+    GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
+    if (!s->split_sync && s->split && s->sort_rows) {
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kseen), size_t(local_shards) * 8 * 4));
+        std::memset(s->h_kseen, 0xFF, size_t(local_shards) * 8 * 4);    // -1: nothing seen yet
+    }
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
@@ -394,7 +406,8 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt),
+                              size_t(gsp::rowx_cnt_stride(shards)) * shards * 4));
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
     }
     if (nccl_id) {
@@ -478,6 +491,7 @@ int gsp_pview_destroy(gsp_pview *s) {
     if (s->h_recv) (void)hipHostFree(s->h_recv);
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->h_kcount) (void)hipHostFree(s->h_kcount);
+    if (s->h_kseen) (void)hipHostFree(s->h_kseen);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -487,7 +501,11 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
     GSP_REQUIRE(s && ticks >= 0, GSP_ERR_INVALID, "gsp_pview_step: bad argument");
     GSP_REQUIRE(s->tick + ticks <= s->p.max_ticks, GSP_ERR_RANGE, "gsp_pview_step: beyond max_ticks");
     GSP_HIP(hipSetDevice(s->device));
-    if (int rc = pview_mirrored_err(s)) return rc;   // an earlier call's ticks overflowed
+    // an earlier call's ticks overflowed: stop here -- except across ranks, whose async mirrors
+    // land at different times (a rank returning here would leave the others in a collective);
+    // the row exchange returns the error on every rank at the same tick instead
+    if (!s->comm)
+        if (int rc = pview_mirrored_err(s)) return rc;
     const int32_t n = s->p.n;
     for (int32_t i = 0; i < ticks; ++i) {
         const int32_t t = s->tick + 1;
@@ -510,6 +528,9 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         for (PvShard &sh : s->local) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
+            if (s->h_kseen)          // never waited on: the next ticks' grid predictions
+                GSP_HIP(hipMemcpyAsync(s->h_kseen + 8 * (&sh - s->local.data()), sh.kcount.p, 8 * 4,
+                                       hipMemcpyDeviceToHost, s->st));
         }
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));

@@ -26,6 +26,8 @@
 //      peers; the row's digest counts go to a per-row record (no global atomics), summed by
 //      pview_digest_kernel.
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
+#include <algorithm>
+
 #include "join_kernels.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
@@ -80,17 +82,43 @@ __device__ inline uint32_t pv_bin(uint32_t v, uint32_t t5, uint32_t th0) {
 // the sender entry of a GOSSIP: hb + 1 and ts = t, or (1, t) when absent (MP1Node.cpp:237-243)
 __device__ inline uint32_t pv_event(uint32_t v, uint32_t t5) { return (((v >> 5) + 1u) << 5) | t5; }
 
+// threadIdx.x as a value the compiler cannot see through: the persistent split kernels loop
+// over rows, and every lane-position value derived from the thread index (slot offsets, LDS
+// addresses) would otherwise be hoisted out of that loop and kept live across the row body,
+// spilling it; an opaque copy per use keeps them per-row temporaries.
+// (Its range [0, NT) is restated, so loops over a lane's slots still unroll.)
+template <int NT>
+__device__ __forceinline__ int32_t pv_tid() {
+    int32_t t = int32_t(threadIdx.x);
+    asm volatile("" : "+v"(t));
+    __builtin_assume(t >= 0 && t < NT);
+    return t;
+}
+
 __device__ inline uint32_t key_id(uint32_t k) { return k >> 11; }
 __device__ inline uint32_t key_src(uint32_t k) { return (k >> 8) & 7u; }
 __device__ inline uint32_t key_slot(uint32_t k) { return k & 255u; }
 
+// The row's barrier: a workgroup barrier for rows of several waves; for a one-wave row (NT =
+// 64) only a wavefront-scope fence, which keeps the compiler from moving LDS accesses across
+// it -- one wave's LDS operations execute in order, so no instruction is needed.
+template <int NT>
+__device__ __forceinline__ void pv_sync() {
+    if constexpr (NT == 64) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    else __syncthreads();
+}
+
 // exclusive block scan over the NT lanes of a row; *total = sum of all lanes.  One barrier:
 // the caller alternates between two s_wave buffers, so a buffer is rewritten only after a
-// later scan's barrier has retired every read of it.
+// later scan's barrier has retired every read of it.  A one-wave row needs neither.
 template <int NT = kPvBlock>
 __device__ inline uint32_t block_scan(uint32_t v, uint32_t *total, uint32_t *s_wave) {
-    const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int32_t lane = pv_tid<NT>() & 63, wave = pv_tid<NT>() >> 6;
     const uint32_t incl = wave_incl_scan(v);
+    if constexpr (NT == 64) {
+        *total = uint32_t(__builtin_amdgcn_readlane(int32_t(incl), 63));
+        return incl - v;
+    }
     if (lane == 63) s_wave[wave] = incl;
     __syncthreads();
     uint32_t before = 0, all = 0;
@@ -149,14 +177,21 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
 // (the last merge level's source) is dead after the tree and holds the (age, hb) eviction
 // bins (1024 u16 counters, words [512, 1024)), the block-scan buffers (8 words at kScan) and,
 // when no eviction is needed, the survivor ids U (words [0, 256)).
+// kKeys = 512 (up to 2 sources, one-wave rows only, 5 KB: 32 rows per CU): the bins take all
+// of keys[cur ^ 1], the kept values follow the kept ids at word 256 of keys[cur], the exact
+// hb histogram spans both halves (one wave: the bins are read before it is zeroed), and
+// block scans need no buffer.
 template <int kKeys>
 struct alignas(16) PvShared {
-    static_assert(kKeys >= 1024 && kKeys <= 2048 && kKeys % 256 == 0, "4 to 8 sources of 256 keys");
-    static constexpr int kHist = kKeys - 1024, kScan = kKeys > 1024 ? kKeys - 8 : 504;
+    static_assert(kKeys == 512 || (kKeys >= 1024 && kKeys <= 2048 && kKeys % 256 == 0),
+                  "2 (one-wave rows) or 4 to 8 sources of 256 keys");
+    static constexpr int kHist = kKeys == 512 ? 0 : kKeys - 1024,
+                         kScan = kKeys == 512 ? 0 : kKeys > 1024 ? kKeys - 8 : 504,
+                         kWValWord = kKeys == 512 ? 256 : 512, kBinWord = kKeys == 512 ? 0 : 512;
     uint32_t keys[2][kKeys];             // merge ping-pong; then the regions above
     uint16_t vals[kKeys];                // values by (source, slot); then survivor values
+    __device__ uint32_t *hist(int cur) { return kKeys == 512 ? &keys[0][0] : keys[cur] + kHist; }
 };
-constexpr int kWValWord = 512, kBinWord = 512;
 
 template <class Sh>
 __device__ inline int32_t lds_word(const Sh &sh, const uint32_t *p) {
@@ -237,7 +272,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     constexpr int kJ = kBlocks - 1;                      // k <= kJ messages in this variant
     constexpr int P = kBlocks * kSlots;
     static_assert(P <= int(sizeof(sh.vals) / 2), "row LDS too small for this variant");
-    const int32_t tid = threadIdx.x;
+    const int32_t tid = pv_tid<NT>();
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
     const uint32_t th0 = t + uint32_t(a.h0);
@@ -332,7 +367,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             if (m > k) sh.keys[1][m * kSlots + slot] = kKeyMax;     // padding for the ping-pong
         }
     }
-    __syncthreads();
+    pv_sync<NT>();
     pm.mark(1);
 
     // ---- 3. merge-path tree: sorted union of every source, ties in message order ------------
@@ -378,7 +413,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             }
             lds_store<Qt>(Y + begt, outk);
         }
-        __syncthreads();
+        pv_sync<NT>();
         cur ^= 1;
     }
     const int32_t beg = tid * Q;                               // the fold's Q keys per lane
@@ -386,7 +421,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     // keys[cur ^ 1] (the last level's source) is dead after the tree: it holds the eviction
     // histogram over (age, hb) bins (1024 u16 counters at words [512, 1024)) and the scan
     // buffers (8 words at Sh::kScan)
-    uint32_t *const bins = sh.keys[cur ^ 1] + kBinWord;
+    uint32_t *const bins = sh.keys[cur ^ 1] + Sh::kBinWord;
     uint32_t *const scan_buf = sh.keys[cur ^ 1] + Sh::kScan;
 #pragma unroll
     for (int i = tid; i < 256; i += NT) reinterpret_cast<uint2 *>(bins)[i] = make_uint2(0u, 0u);
@@ -572,7 +607,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     // order.  A boundary bin e < 31 holds one (age, hb); the last bin of an age (e >= 31)
     // can hold several hb values -- then the exact boundary hb comes from an hb histogram.
     if (evict) {
-        __syncthreads();                                   // bin histogram complete
+        pv_sync<NT>();                                   // bin histogram complete
         const int32_t lane = tid & 63;
         uint32_t bstar, need, at;
         {   // every wave: lane l sums bins [16 l, 16 l + 16), the lane holding the V-th entry
@@ -601,14 +636,14 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         const uint32_t astar = bstar >> 5;
         uint32_t hstar = th0 - astar - (bstar & 31u), need2 = need;
         if (tie && (bstar & 31u) == 31u) {                               // block-uniform: exact hb boundary
-            uint32_t *hist = sh.keys[cur] + Sh::kHist;     // 2048 hb bins, u16 pairs; C is dead
+            uint32_t *hist = sh.hist(cur);                 // 2048 hb bins, u16 pairs; C is dead
             for (int32_t i = tid; i < 1024; i += NT) hist[i] = 0;
-            __syncthreads();
+            pv_sync<NT>();
             for_each([&](uint32_t v, uint32_t, uint32_t b) {
                 if (b == bstar)
                     atomicAdd(&hist[(v >> 5) >> 1], 1u << (((v >> 5) & 1u) * 16u));
             });
-            __syncthreads();
+            pv_sync<NT>();
             // every wave: lane l sums hb bins 2047 - 32l - 31 .. 2047 - 32l (descending lanes),
             // the lane holding the need-th largest walks its bins
             const uint16_t *h16 = reinterpret_cast<const uint16_t *>(hist);
@@ -649,7 +684,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
         uint32_t *Wid = sh.keys[cur];
-        uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + kWValWord);
+        uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + Sh::kWValWord);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
         const bool ev_on = (kExt & kExtEv) && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
         if (ev_on) {
@@ -683,7 +718,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     ro.evicts = evicts;
     ro.merged = merged;
     ro.hsum = hsum;
-    __syncthreads();
+    pv_sync<NT>();
 }
 
 // ---- 6. write the view and the row's digest record (peers: pview_send_kernel) -------------
@@ -694,7 +729,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
 template <int NT, class Sh>
 __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_t lr,
                                           int32_t k, int32_t k_all, bool init, const RowOut &ro) {
-    const int32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int32_t tid = pv_tid<NT>(), lane = tid & 63, wave = tid >> 6;
     const int32_t V = a.view, len = ro.len;
     const uint32_t t = uint32_t(a.tick);
     const uint32_t *ids = &sh.keys[0][0] + ro.ids_off;
@@ -728,8 +763,9 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_
         rec[0] = make_ulonglong2(w0, w1);
         if (wave == 0) rec[1].x = h;                  // w3 belongs to the send kernel
         else rec[1] = make_ulonglong2(h, 0ull);
-        if (NT == 128) {
-            ulonglong2 *z = reinterpret_cast<ulonglong2 *>(a.rowdig + (int64_t(lr) * 4 + wave + 2) * 4);
+#pragma unroll
+        for (int w = NT / 64; w < 4; w += NT / 64) {     // the records of waves this row lacks
+            ulonglong2 *z = reinterpret_cast<ulonglong2 *>(a.rowdig + (int64_t(lr) * 4 + wave + w) * 4);
             z[0] = z[1] = make_ulonglong2(0ull, 0ull);
         }
     }
@@ -756,7 +792,7 @@ __device__ __forceinline__ int32_t pv_row_of(const PviewTickArgs &a, int32_t b) 
 template <int kExt, int NT, int kQlo, int kQhi, class Sh>
 __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t lr) {
     constexpr int SL = kSlots / NT;
-    const int32_t tid = threadIdx.x, lane = tid & 63;
+    const int32_t tid = pv_tid<NT>(), lane = tid & 63;
     const int32_t r = a.row0 + lr;
     uint64_t ent0[SL];
 #pragma unroll
@@ -858,13 +894,12 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
     pv_finish<kPvBlock>(a, sh, lr, 0, 0, true, ro);
 }
 
-// kWaves: minimum waves per SIMD the register allocation must allow (8 = 8 rows per CU, the
-// LDS limit; 7 = the allocator's own choice).  A/B switch: GSP_PV_WAVES.  One row per
-// workgroup: a software-pipelined variant (the next row's record, own view and first sender
-// views requested while the current row merged, two rows per workgroup) measured 4-8 % slower
-// -- other resident rows already hide the HBM round trips.
-template <int kWaves, int kExt>
-__global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickArgs a) {
+// The one-kernel form (GSP_PV_SPLIT=0; every row a 256-lane row in 20 KB, any k).  One row
+// per workgroup: a software-pipelined variant (the next row's record, own view and first
+// sender views requested while the current row merged, two rows per workgroup) measured 4-8 %
+// slower -- other resident rows already hide the HBM round trips.
+template <int kExt>
+__global__ void __launch_bounds__(kPvBlock, 8) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared<kMaxKeys> sh;
     pv_row<kExt, kPvBlock, 0, 7>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
 }
@@ -872,19 +907,68 @@ __global__ void __launch_bounds__(kPvBlock, kWaves) pview_tick_kernel(PviewTickA
 // Split form (rows bucketed by k, a.order set): the rows that merge at most 3 messages
 // (kQhi = 3: at most 4 sources, 1024 keys) run as 128-lane rows in 10 KB of LDS -- 16 rows
 // per CU instead of 8, two waves per row instead of four, each lane holding two slots of
-// every source -- and the rest as 256-lane rows.  The bucket sizes are on the device, so
-// each kernel is launched over every row and the workgroups past its buckets' rows return
-// at once (a grid-stride loop instead kept the row body's loop-invariant values live across
-// it and spilled).
+// every source -- k = 4 and k = 5 as 128-lane rows in 12.5 / 15 KB, k = 6, 7 as 256-lane
+// rows in 20 KB.  Workgroup b runs the b-th row of its buckets' k-descending order; rows at
+// or past the grid belong to pview_tick_overflow_kernel (the grid is either the exact bucket
+// size, read back by the host, or the host's prediction from the last counts it has seen).
 template <int kExt, int NT, int kQlo, int kQhi, int kMinWaves = 8>
 __global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTickArgs a) {
-    __shared__ PvShared<kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots> sh;
+    __shared__ PvShared<NT == 64 ? 512 : kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots> sh;
+    static_assert(NT != 64 || kQhi <= 1, "one-wave rows hold at most 2 sources");
     int32_t total = 0;
 #pragma unroll
     for (int q = kQlo; q <= kQhi; ++q) total += a.kcount[q];
     const int32_t b = int32_t(blockIdx.x);
     if (b >= total) return;
     pv_row<kExt, NT, kQlo, kQhi>(a, sh, pv_row_of<kQlo, kQhi>(a, b));
+}
+
+// The split kernels' k ranges, in launch order (launch_pview_tick).
+#ifdef GSP_PV_NT64
+constexpr int kPvRanges = 5;
+__device__ __forceinline__ int32_t pv_range_lo(int32_t j) { return j == 0 ? 6 : j == 1 ? 5 : j == 2 ? 4 : j == 3 ? 2 : 0; }
+__device__ __forceinline__ int32_t pv_range_hi(int32_t j) { return j == 0 ? 7 : j == 1 ? 5 : j == 2 ? 4 : j == 3 ? 3 : 1; }
+#else
+constexpr int kPvRanges = 4;
+__device__ __forceinline__ int32_t pv_range_lo(int32_t j) { return j == 0 ? 6 : j == 1 ? 5 : j == 2 ? 4 : 0; }
+__device__ __forceinline__ int32_t pv_range_hi(int32_t j) { return j == 0 ? 7 : j == 1 ? 5 : j == 2 ? 4 : 3; }
+#endif
+
+// The rows of every split range at or past that kernel's grid (a.split_grid[j]): the grids the
+// host predicted were too small for this tick's buckets.  A fixed grid; each workgroup runs
+// such rows b, b + grid, ... as 256-lane rows (any k) until none is left -- usually none, and
+// the kernel costs one short launch.  This is what lets the host launch a tick without
+// reading its bucket sizes back: gsp_pview_step queues ticks with no host wait.
+template <int kExt>
+__global__ void __launch_bounds__(kPvBlock, 8) pview_tick_overflow_kernel(PviewTickArgs a) {
+    __shared__ PvShared<kMaxKeys> sh;
+    int32_t over[kPvRanges], total = 0;
+#pragma unroll
+    for (int j = 0; j < kPvRanges; ++j) {
+        int32_t c = 0;
+        for (int32_t q = pv_range_lo(j); q <= pv_range_hi(j); ++q) c += a.kcount[q];
+        over[j] = c > a.split_grid[j] ? c - a.split_grid[j] : 0;
+        total += over[j];
+    }
+    for (int32_t b = int32_t(blockIdx.x); b < total; b += int32_t(gridDim.x)) {
+        int32_t j = 0, off = b;                  // block-uniform: the range and the offset
+#pragma unroll
+        for (int q = 0; q < kPvRanges - 1; ++q)
+            if (j == q && off >= over[q]) { off -= over[q]; j = q + 1; }
+        int32_t pos = a.split_grid[j] + off;     // the position in the range's k-descending order
+        int32_t q = pv_range_hi(j);
+        for (; q > pv_range_lo(j); --q) {
+            const int32_t c = a.kcount[q];
+            if (pos < c) break;
+            pos -= c;
+        }
+        // the scalars every row derives its constants from, opaque per row (as pv_tid): hoisted
+        // out of this loop they would stay live across the row body
+        PviewTickArgs ai = a;
+        asm volatile("" : "+s"(ai.tick), "+s"(ai.h0), "+s"(ai.tremove), "+s"(ai.view));
+        pv_row<kExt, kPvBlock, 0, 7>(ai, sh, ai.order[int64_t(q) * ai.rows + pos]);
+        __syncthreads();                         // the row's LDS is read by its view write
+    }
 }
 
 // One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
@@ -1112,64 +1196,89 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     const int ext = ((a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr) ? kExtPol : 0) |
                     (a.ev.buf != nullptr ? kExtEv : 0);
     if (a.order && a.split) {
-        // split form: rows with k >= 4 as 256-lane rows, k <= 3 as 128-lane rows
-        unsigned gb = unsigned(a.rows), gs = unsigned(a.rows), g4 = unsigned(a.rows), g5 = unsigned(a.rows),
-                 g67 = unsigned(a.rows), g0 = unsigned(a.rows), g13 = unsigned(a.rows);
-        if (a.kcount_host) {                          // exact grids: the counts, synchronously
+        // split form: k = 6, 7 / k = 5 / k = 4 / k <= 3 (pview_tick_split_kernel), in this order
+        // (the heavy rows first).  Grids: the exact bucket sizes, read back synchronously
+        // (a.kcount_host, GSP_PV_SPLITSYNC=1), or -- by default, no host wait -- predicted from
+        // the last counts the host has seen (a.kcount_seen, copied back asynchronously each
+        // tick; 6 % + 256 of margin), every row past a grid run by the overflow kernel.
+        PviewTickArgs b = a;
+        int32_t c[8];
+        const bool exact = a.kcount_host != nullptr;
+        if (exact) {
             if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return hipGetLastError();
-            const int32_t *c = a.kcount_host;
-            gb = unsigned(c[4] + c[5] + c[6] + c[7]);
-            gs = unsigned(c[0] + c[1] + c[2] + c[3]);
-            g4 = unsigned(c[4]);
-            g5 = unsigned(c[5]);
-            g67 = unsigned(c[6] + c[7]);
-            g0 = unsigned(c[0]);
-            g13 = unsigned(c[1] + c[2] + c[3]);
+            for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
+        } else {
+            for (int q = 0; q < 8; ++q) c[q] = a.kcount_seen ? a.kcount_seen[q] : -1;
         }
-        // split bits: 1 on, 2 small rows first, 8 the k = 4 and k = 5 rows as 128-lane rows in
-        // 12.5 / 15 KB (12 / 10 rows per CU) and k = 6, 7 as 256-lane rows, 32 the k = 0 rows in
-        // a kernel of their own.  A/B (ticks 6-15, one box): 1 -> 9 -1.6 %, 41 -0.7 %; dropped:
-        // every k >= 4 row as a 128-lane row in 20 KB (8 rows, 4 waves per SIMD) +8.7 %, only
-        // k = 6, 7 so +6 %, a one-wave k = 0 kernel without LDS (scan + compaction) +7 %, the
-        // k >= 4 kernels on a second stream beside the small rows' (fork / join events) ±0.5 %.
-        auto launch = [&](auto big, auto k4, auto k5, auto k67, auto small, auto k0, auto k13) {
-            auto sm = [&] { if (a.split & 32) { k13(); k0(); } else small(); };
-            if (a.split & 2) sm();
-            if (a.split & 8) { k67(); k5(); k4(); }
-            else big();
-            if (!(a.split & 2)) sm();
+        auto grid = [&](int lo, int hi) {
+            int64_t g = 0;
+            for (int q = lo; q <= hi; ++q) {
+                if (c[q] < 0 || c[q] > a.rows) {                   // nothing seen yet: every row
+                    g = a.rows;
+                    break;
+                }
+                g += c[q];
+            }
+            if (!exact) g += g / 16 + 256;
+            if (!exact && a.test_grid_cap > 0 && g > a.test_grid_cap) g = a.test_grid_cap;
+            return int32_t(g < a.rows ? g : a.rows);
         };
-#define GSP_PV_SPLIT_LAUNCH(E)                                                                        \
-    launch([&] { if (gb) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 4, 7>), dim3(gb), dim3(256), 0, st, a); }, \
-           [&] { if (g4) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(g4), dim3(128), 0, st, a); }, \
-           [&] { if (g5) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(g5), dim3(128), 0, st, a); }, \
-           [&] { if (g67) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(g67), dim3(256), 0, st, a); }, \
-           [&] { if (gs) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(gs), dim3(128), 0, st, a); }, \
-           [&] { if (g0) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 0>), dim3(g0), dim3(128), 0, st, a); }, \
-           [&] { if (g13) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 1, 3>), dim3(g13), dim3(128), 0, st, a); })
+        b.split_grid[0] = grid(6, 7);
+        b.split_grid[1] = grid(5, 5);
+        b.split_grid[2] = grid(4, 4);
+#ifdef GSP_PV_NT64
+        b.split_grid[3] = grid(2, 3);
+        b.split_grid[4] = grid(0, 1);
+#else
+        b.split_grid[3] = grid(0, 3);
+#endif
+        const int32_t cus = a.cus > 0 ? a.cus : 256;
+        const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
+#ifdef GSP_PV_NT64   // k = 2, 3 as 128-lane rows, k = 0, 1 as one-wave rows in 5 KB (32 per CU)
+#define GSP_PV_SMALL_ROWS(E)                                                                              \
+        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 2, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b); \
+        if (b.split_grid[4]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 64, 0, 1>), dim3(b.split_grid[4]), dim3(64), 0, st, b);
+#else
+#define GSP_PV_SMALL_ROWS(E)                                                                              \
+        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
+#endif
+#define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
+    do {                                                                                                  \
+        if (b.split_grid[0]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(b.split_grid[0]), dim3(256), 0, st, b); \
+        if (b.split_grid[1]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b); \
+        if (b.split_grid[2]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b); \
+        GSP_PV_SMALL_ROWS(E)                                                                              \
+        if (!exact) hipLaunchKernelGGL((pview_tick_overflow_kernel<E>), dim3(gov), dim3(kPvBlock), 0, st, b); \
+    } while (0)
+#ifdef GSP_PV_EXP_PLAIN_ONLY   // experiments: the plain protocol's kernels only (fast builds)
+        if (ext != 0) return hipErrorNotSupported;
+        GSP_PV_SPLIT_LAUNCH(0);
+#else
         switch (ext) {
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
             case kExtEv: GSP_PV_SPLIT_LAUNCH(kExtEv); break;
             case kExtPol: GSP_PV_SPLIT_LAUNCH(kExtPol); break;
             default: GSP_PV_SPLIT_LAUNCH(kExtPol | kExtEv); break;
         }
+#endif
 #undef GSP_PV_SPLIT_LAUNCH
-        launch_send_and_digest(a, st);
+#undef GSP_PV_SMALL_ROWS
+        launch_send_and_digest(b, st);
         return hipGetLastError();
     }
-    const bool w8 = a.waves == 8;
+#ifdef GSP_PV_EXP_PLAIN_ONLY
+    if (ext != 0) return hipErrorNotSupported;
+    hipLaunchKernelGGL((pview_tick_kernel<0>), g, blk, 0, st, a);
+#else
     switch (ext) {
-        case 0: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, 0>), g, blk, 0, st, a);
-                else hipLaunchKernelGGL((pview_tick_kernel<7, 0>), g, blk, 0, st, a); break;
-        case kExtEv: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtEv>), g, blk, 0, st, a);
-                     else hipLaunchKernelGGL((pview_tick_kernel<7, kExtEv>), g, blk, 0, st, a); break;
-        case kExtPol: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtPol>), g, blk, 0, st, a);
-                      else hipLaunchKernelGGL((pview_tick_kernel<7, kExtPol>), g, blk, 0, st, a); break;
-        default: if (w8) hipLaunchKernelGGL((pview_tick_kernel<8, kExtPol | kExtEv>), g, blk, 0, st, a);
-                 else hipLaunchKernelGGL((pview_tick_kernel<7, kExtPol | kExtEv>), g, blk, 0, st, a); break;
+        case 0: hipLaunchKernelGGL((pview_tick_kernel<0>), g, blk, 0, st, a); break;
+        case kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtEv>), g, blk, 0, st, a); break;
+        case kExtPol: hipLaunchKernelGGL((pview_tick_kernel<kExtPol>), g, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((pview_tick_kernel<kExtPol | kExtEv>), g, blk, 0, st, a); break;
     }
+#endif
     launch_send_and_digest(a, st);
     return hipGetLastError();
 }

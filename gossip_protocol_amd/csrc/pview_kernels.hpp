@@ -56,10 +56,16 @@ struct PviewTickArgs {
     const int32_t *order;        // [8][rows]: the rows of each k; workgroup b runs the b-th row
                                  // of the k-descending order (one code variant per CU stretch)
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
-    int32_t waves;               // register budget variant of the tick kernel (7 or 8)
-    int32_t split;               // with order set: k <= 3 rows as 128-lane rows (two kernels)
-    int32_t *kcount_host;        // pinned [8], or null: the split kernels' grids are the exact
-                                 // bucket sizes, read back with a stream sync (A/B: GSP_PV_SPLITSYNC)
+    int32_t split;               // with order set: rows bucketed by k into four kernels
+    int32_t *kcount_host;        // pinned [8]: the split kernels' grids are the exact bucket
+                                 // sizes, read back with a stream sync (GSP_PV_SPLITSYNC=1), or
+                                 // null: predicted grids + the overflow kernel, no host wait
+    const int32_t *kcount_seen;  // host, pinned [8]: the last bucket sizes copied back (any
+                                 // value is safe: it only sizes grids), or null
+    int32_t cus;                 // compute units of the device (overflow kernel grid)
+    int32_t split_grid[5];       // set by launch_pview_tick: the split kernels' grids
+    int32_t test_grid_cap;       // tests only (GSP_TEST_PV_GRID_CAP): cap on every predicted
+                                 // split grid, so the overflow kernel runs most rows (0: none)
 };
 constexpr int kPvProfPhases = 10;
 

@@ -22,8 +22,9 @@ hipError_t RowxBufs::alloc(int32_t shards, int64_t pair_cap, int64_t msg_cap, in
                            int64_t csr_cap, hipStream_t st) {
     const size_t G = size_t(shards), R = size_t(shards > 1 ? shards - 1 : 1);   // regions
     hipError_t e;
-    if ((e = cnt.alloc(2 * G)) != hipSuccess) return e;
-    if ((e = cnt_all.alloc(2 * G * G)) != hipSuccess) return e;
+    const size_t S = size_t(rowx_cnt_stride(shards));
+    if ((e = cnt.alloc(S)) != hipSuccess) return e;
+    if ((e = cnt_all.alloc(S * G)) != hipSuccess) return e;
     if ((e = recv_msgs.alloc(G)) != hipSuccess) return e;
     if ((e = pair_row.alloc(R * size_t(pair_cap))) != hipSuccess) return e;
     if ((e = csr_slot.alloc(size_t(csr_cap))) != hipSuccess) return e;
@@ -43,10 +44,11 @@ void RowxBufs::release() {
 }
 
 int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *bytes) {
-    const int32_t G = job.shards, W = job.row_words, F = job.fanout;
+    const int32_t G = job.shards, W = job.row_words, F = job.fanout, S = rowx_cnt_stride(G);
     hipStream_t st = job.st;
     for (RowxShard &sh : local) {
         GSP_HIP(hipMemsetAsync(sh.x->cnt.p, 0, size_t(2 * G) * 4, st));
+        GSP_HIP(hipMemcpyAsync(sh.x->cnt.p + 2 * G, sh.err, 4, hipMemcpyDeviceToDevice, st));
         RowxArgs a{};
         a.n = job.n;
         a.shards = G;
@@ -67,19 +69,23 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
         GSP_HIP(launch_rowx_pack(a, st));
         GSP_HIP(launch_rowx_gather(a, st));
     }
-    // counts of every shard -> cnt_all[G][2G] of the first local shard, read by the host
+    // counts of every shard -> cnt_all[G][2G + 1] of the first local shard, read by the host
     RowxBufs &x0 = *local[0].x;
     if (job.comm) {
-        GSP_NCCL(ncclAllGather(x0.cnt.p, x0.cnt_all.p, size_t(2 * G), ncclInt32, job.comm, st));
+        GSP_NCCL(ncclAllGather(x0.cnt.p, x0.cnt_all.p, size_t(S), ncclInt32, job.comm, st));
     } else {
         for (RowxShard &src : local)
-            GSP_HIP(hipMemcpyAsync(x0.cnt_all.p + size_t(src.g) * 2 * G, src.x->cnt.p,
-                                   size_t(2 * G) * 4, hipMemcpyDeviceToDevice, st));
+            GSP_HIP(hipMemcpyAsync(x0.cnt_all.p + size_t(src.g) * S, src.x->cnt.p, size_t(S) * 4,
+                                   hipMemcpyDeviceToDevice, st));
     }
-    GSP_HIP(hipMemcpyAsync(job.h_cnt, x0.cnt_all.p, size_t(2 * G) * G * 4, hipMemcpyDeviceToHost, st));
+    GSP_HIP(hipMemcpyAsync(job.h_cnt, x0.cnt_all.p, size_t(S) * G * 4, hipMemcpyDeviceToHost, st));
     GSP_HIP(hipStreamSynchronize(st));
-    auto pairs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * 2 * G + h]); };
-    auto msgs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * 2 * G + G + h]); };
+    auto pairs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * S + h]); };
+    auto msgs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * S + G + h]); };
+    for (int32_t g = 0; g < G; ++g)       // the same all-gathered flags on every rank
+        GSP_REQUIRE(job.h_cnt[size_t(g) * S + 2 * G] == 0, GSP_ERR_CAPACITY,
+                    "a receiver of shard %d got more messages than the kernel's segment bound at "
+                    "tick %d; ticks after it did not run", g, job.h_cnt[size_t(g) * S + 2 * G]);
     for (int32_t g = 0; g < G; ++g)
         for (int32_t h = 0; h < G; ++h)
             GSP_REQUIRE(pairs(g, h) <= job.pair_cap && msgs(g, h) <= job.msg_cap, GSP_ERR_CAPACITY,

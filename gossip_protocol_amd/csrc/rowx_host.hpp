@@ -30,6 +30,7 @@ struct RowxShard {
     const uint64_t *table;        // this shard's rows of that tick, row_words words each
     int32_t *deg;                 // [n] destination counts of that tick (zeroed on return)
     int32_t *off, *fill, *csr_src, *tile_sum;
+    const int32_t *err;           // the shard's capacity flag (0, or the tick that overflowed)
     RowxBufs *x;
 };
 
@@ -38,11 +39,16 @@ struct RowxJob {
     int64_t pair_cap, msg_cap;
     ncclComm_t comm;              // one shard per process; null: every shard is local
     hipStream_t st;
-    int32_t *h_cnt;               // pinned [G][2G]
+    int32_t *h_cnt;               // pinned [G][2G + 1]: pairs, records, capacity flag per shard
     int32_t *h_recv;              // pinned [local shards][G]
 };
 
-// Returns a gsp_status; *bytes += bytes the local shards sent to other shards.
+// Counts per shard in the all-gather: G pair counts, G record counts, its capacity flag.
+inline int32_t rowx_cnt_stride(int32_t shards) { return 2 * shards + 1; }
+
+// Returns a gsp_status; *bytes += bytes the local shards sent to other shards.  Every shard's
+// capacity flag travels with the counts, so every rank returns GSP_ERR_CAPACITY at the same
+// point (before any send / receive) once any shard's receiver overflowed.
 int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *bytes);
 
 }  // namespace gsp

@@ -151,7 +151,7 @@ struct gsp_scale {
         a.ping = (shared ? s0 : sh).ping.p;
         a.bitmap = shared ? s0.bitmap.p + size_t(sh.g - rank) * size_t(p.n) * size_t(stride / 8) : sh.bitmap.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kDigSlots * gsp::kDigFields;
-        a.err = sh.err.p;
+        a.err = local[0].err.p;        // one flag for every shard held here
         a.max_segment = max_segment;
         a.ev = sh.ev.args();
         return a;
@@ -246,7 +246,8 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     if (s->sliced && (!s->shared || &sh == &s->local[0])) {
         GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
         GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards * (s->shared ? 2 : 1)));
-        GSP_HIP(sh.picks.alloc(size_t(n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0))));
+        // + 1: the capacity flag rides the all-reduce MAX of the picks (exchange_picks)
+        GSP_HIP(sh.picks.alloc(size_t(n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0)) + 1));
         // shared: every local shard's bitmap, one region each (the resolve reads them all)
         GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8) * (s->shared ? s->local.size() : 1)));
     }
@@ -305,8 +306,12 @@ int exchange_counts(gsp_scale *s, int32_t t) {
 int exchange_picks(gsp_scale *s) {
     const size_t cnt = size_t(s->p.n) * (s->p.fanout + (s->p.swim > 0 ? 1 : 0));
     if (s->comm) {
+        // the capacity flag (0, or the tick that overflowed) rides along in slot cnt, so every
+        // rank's next tick kernels stop together and every rank's sync reports it
         Shard &sh = s->local[0];
-        GSP_NCCL(ncclAllReduce(sh.picks.p, sh.picks.p, cnt, ncclInt32, ncclMax, s->comm, s->st));
+        GSP_HIP(hipMemcpyAsync(sh.picks.p + cnt, sh.err.p, 4, hipMemcpyDeviceToDevice, s->st));
+        GSP_NCCL(ncclAllReduce(sh.picks.p, sh.picks.p, cnt + 1, ncclInt32, ncclMax, s->comm, s->st));
+        GSP_HIP(hipMemcpyAsync(sh.err.p, sh.picks.p + cnt, 4, hipMemcpyDeviceToDevice, s->st));
         return GSP_OK;
     }
     Shard &root = s->local[0];
@@ -380,13 +385,17 @@ int exchange_rows(gsp_scale *s, int32_t t_sent) {
     for (Shard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p,
                                    reinterpret_cast<const uint64_t *>(sh.table[t_sent & 1].p),
-                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p, &sh.x});
+                                   sh.deg.p, sh.off.p, sh.fill.p, sh.csr_src.p, sh.tile_sum.p,
+                                   s->local[0].err.p, &sh.x});
     return gsp::rowx_exchange(job, v, &s->perf.xgmi_bytes);
 }
 
-// The capacity flags as last mirrored to the host (no synchronisation): a receiver with more
-// than max_segment messages sets its shard's flag to the tick, and every later tick kernel
-// returns at once, so the job's state stays that of the tick before the overflow.
+// The capacity flag as last mirrored to the host (no synchronisation): a receiver with more
+// than max_segment messages sets the flag to the tick, and every later tick kernel returns at
+// once, so the job's state stays that of the tick before the overflow.  Every shard held by
+// this engine reads one flag (shard 0's); with a communicator the flag is exchanged each tick
+// (columns: inside the picks all-reduce; rows: with the exchange counts), so all ranks stop
+// together.
 int mirrored_err(gsp_scale *s) {
     for (size_t i = 0; i < s->local.size(); ++i)
         GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
@@ -543,7 +552,8 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt), size_t(2 * shards) * shards * 4));
+        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt),
+                              size_t(gsp::rowx_cnt_stride(shards)) * shards * 4));
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
     }
     if (nccl_id) {
@@ -642,7 +652,13 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
     GSP_REQUIRE(s->tick + ticks <= s->p.max_ticks, GSP_ERR_RANGE,
                 "gsp_scale_step: tick %d beyond max_ticks %d", s->tick + ticks, s->p.max_ticks);
     GSP_HIP(hipSetDevice(s->device));
-    if (int rc = mirrored_err(s)) return rc;     // an earlier call's ticks overflowed
+    // an earlier call's ticks overflowed: one process stops here at once; ranks of a
+    // communicator do not (the async mirror lands at different times on different ranks, and a
+    // rank that returned would leave the others in a collective) -- their kernels already run
+    // no row, the row exchange returns the error on every rank at the same tick, and sync
+    // reports it
+    if (!s->comm)
+        if (int rc = mirrored_err(s)) return rc;
     const int32_t n = s->p.n;
     const int64_t slots = int64_t(n) * s->p.fanout;
     for (int32_t i = 0; i < ticks; ++i) {

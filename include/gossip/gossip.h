@@ -301,7 +301,8 @@ typedef struct {
  * them (Params.cpp:22-25; every reference testcase parses unchanged) mapped as its driver uses
  * them -- n = MAX_NNB, SINGLE_FAILURE 1: one Philox-chosen node crashes at t = 100, 0: n/2
  * contiguous nodes (Application.cpp:180-196), DROP_MSG: drop_pct = (int)(MSG_DROP_PROB * 100)
- * in [50, 300) (EmulNet.cpp:91, Application.cpp:177/198), STEP_RATE 0.25, 700 ticks -- then
+ * for the sends of ticks [51, 301) (EmulNet.cpp:91; Application.cpp:177/198 set and clear
+ * dropmsg at the end of t = 50 / 300), STEP_RATE 0.25, 700 ticks -- then
  * optional "KEY: value" lines: SCALE_N FANOUT TREMOVE TFAIL SWIM H0 SEED TICKS STEP_RATE
  * INTRO_LIST DROP_PCT DROP_WINDOW(from until) FAIL(tick mode ppm, repeatable) EVENTS EVENT_CAP,
  * and for the partial view VIEW INBOX.  Unknown keys fail with GSP_ERR_INVALID. */
@@ -390,9 +391,9 @@ int gsp_scale_hip_stream(gsp_scale *s, void **stream);
  * staged in LDS and reserved in the ring at once; the ring is 256 stripes (row % 256), each
  * with its own counter, so reservations do not queue on one address.
  * drain: copies the records of every tick since the last drain (stripe by stripe, device
- * order within a stripe) into buf (at most cap), sets *n to the number held and *lost to the
- * records a full stripe could not hold, and empties the ring; buf = NULL only counts (the
- * ring is kept).
+ * order within a stripe) into buf, at most cap of them, sets *n to the number copied and
+ * *lost to the records a full stripe could not hold plus those past cap, and empties the
+ * ring; buf = NULL only counts (*n = the records held; the ring is kept).
  * ---------------------------------------------------------------------------------- */
 int gsp_scale_drain_events(gsp_scale *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
 /* Appends event records as the reference's dbg.log lines (Log.cpp:44-130): "\n <r> [t] Node

@@ -142,3 +142,27 @@ def test_events_off_refuses_drain():
     with ScaleEngine(64, max_ticks=2, fanout=3, seed=5) as eng:
         with pytest.raises(Exception, match="records no events"):
             eng.drain_events()
+
+
+def test_drain_with_small_buffer_counts_the_rest_as_lost():
+    """gsp_scale_drain_events with cap below the records held: *n = the records copied (cap),
+    the rest count as lost, and the ring is emptied (gossip.h)."""
+    import ctypes
+    n, ticks = 400, 8
+    with ScaleEngine(n, max_ticks=ticks, fanout=3, seed=5, fail_mode=RANDOM, fail_tick=2,
+                     fail_ppm=100000, tremove=3, events=True) as eng:
+        eng.drain_events()
+        eng.step(ticks)
+        fn = _lib.lib().gsp_scale_drain_events
+        held, lost = ctypes.c_int64(), ctypes.c_int64()
+        assert fn(eng._h, None, 0, ctypes.byref(held), ctypes.byref(lost)) == 0
+        assert held.value > 10 and lost.value == 0
+        cap = held.value // 3
+        buf = np.zeros(held.value, np.uint64)
+        got, lost = ctypes.c_int64(), ctypes.c_int64()
+        assert fn(eng._h, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), cap,
+                  ctypes.byref(got), ctypes.byref(lost)) == 0
+        assert got.value == cap and lost.value == held.value - cap
+        assert np.all(buf[cap:] == 0) and np.all(buf[:cap] != 0)
+        rec, lost2 = eng.drain_events()
+        assert len(rec) == 0 and lost2 == 0

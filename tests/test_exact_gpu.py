@@ -33,6 +33,24 @@ def test_exact_bitexact_vs_reference(tmp_path, mode, conf, seed):
     assert st.batches == 700 and st.node_rounds > 0 and st.device_ms > 0
 
 
+def test_conf_drop_window_is_the_exact_drivers(tmp_path, monkeypatch):
+    """The drop window the scale engines map a reference .conf's DROP_MSG to
+    (gsp_scale_params_from_conf) is exactly the set of ticks whose sends the byte-exact driver
+    runs with dropmsg = 1 (Application.cpp:177, 198: set / cleared at the END of t = 50 / 300)."""
+    from gossip_protocol_amd.scale import params_from_conf as scale_conf
+    seen = {}
+    orig = exact.Engine.process
+
+    def record(self, tick, order, ops, dropmsg):
+        seen[tick] = dropmsg
+        return orig(self, tick, order, ops, dropmsg)
+    monkeypatch.setattr(exact.Engine, "process", record)
+    exact.run_application(conf_path("msgdropsinglefailure"), 5, "glibc", str(tmp_path))
+    p = scale_conf(conf_path("msgdropsinglefailure"))
+    assert sorted(t for t, d in seen.items() if d) == \
+        list(range(p.policy.drop_from, p.policy.drop_until))
+
+
 def test_exact_stale_payload_is_rejected():
     """A GOSSIP whose sender re-ran before delivery cannot be replayed: loud error."""
     p = exact.params_from_conf(conf_path("singlefailure"))

@@ -57,16 +57,18 @@ def test_pview_eviction_bins_match_oracle(case):
     _run_case(case[:-1], h0=case[-1])
 
 
-# the tick kernel's launch forms (GSP_PV_SPLIT: 0 one 256-lane kernel for every row; 1 rows
-# merging <= 3 messages as 128-lane rows; 9 also k = 4 and k = 5 as 128-lane rows in their own
-# LDS size; 41 the k = 0 rows in a kernel of their own;
-# GSP_PV_SPLITSYNC=0: grids of every row instead of the bucket sizes read back)
-@pytest.mark.parametrize("form", ["0:1", "1:1", "9:1", "9:0", "11:1", "41:1"])
+# the tick kernel's launch forms -- GSP_PV_SPLIT: 0 one 256-lane kernel for every row, 1 rows
+# bucketed by k into four kernels; GSP_PV_SPLITSYNC: 1 exact grids (the bucket sizes read back
+# each tick), 0 grids predicted from the last sizes seen + the overflow kernel (the default, no
+# host wait); GSP_TEST_PV_GRID_CAP caps the predicted grids, so the overflow kernel runs most
+# rows (3) or the tail of every bucket (50)
+@pytest.mark.parametrize("form", ["0:1:0", "1:1:0", "1:0:0", "1:0:3", "1:0:50"])
 @pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4]], ids=lambda c: "n%d_v%d" % c[:2])
 def test_pview_kernel_forms_match_oracle(case, form, monkeypatch):
-    split, sync = form.split(":")
+    split, sync, cap = form.split(":")
     monkeypatch.setenv("GSP_PV_SPLIT", split)
     monkeypatch.setenv("GSP_PV_SPLITSYNC", sync)
+    monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
     _run_case(case)
 
 
@@ -169,6 +171,27 @@ def test_pview_capacity_error_stops_the_job(monkeypatch):
     with PviewEngine(300, view=64, fanout=8, inbox=7, max_ticks=10) as eng:
         eng.step(3)
         assert eng.digest(3)["node_rounds"] == 300
+
+
+@pytest.mark.parametrize("form", ["group3", "rank"])
+def test_pview_capacity_error_stops_every_shard(monkeypatch, form):
+    """An overflow in one row shard stops the whole job: an in-process group's shards read one
+    flag, and a rank's flag travels with the row-exchange counts, so every rank returns the
+    error at the same tick instead of one rank leaving the others in a collective."""
+    from gossip_protocol_amd._lib import GspError
+    from gossip_protocol_amd.scale import nccl_unique_id
+    monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
+    kw = dict(view=64, fanout=8, inbox=7, max_ticks=10)
+    kw.update(group=3) if form == "group3" else kw.update(rank=0, world=1, nccl_id=nccl_unique_id())
+    with PviewEngine(300, **kw) as eng:
+        eng.step(1)
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.sync()
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.step(1)
+            eng.sync()
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.digest(1)
 
 
 def test_pview_full_size_properties():

@@ -510,3 +510,31 @@ def test_config4_one_gpu_32_tiles_properties():
             e[r] = 0
             e = np.where((e != 0) & (((t5 - e) & 31) >= tr), 0, e)
             assert np.array_equal(e.astype(np.uint16), eng.row(r)), "row %d" % r
+
+
+@pytest.mark.parametrize("form", ["rows3", "columns2", "rank_columns", "rank_rows"])
+def test_capacity_error_stops_every_shard(monkeypatch, form):
+    """A receiver overflow stops every shard of the job together: the shards of
+    an in-process group read one flag; ranks of a communicator exchange it each tick (columns:
+    inside the picks all-reduce; rows: with the row-exchange counts) and never return early
+    from a step on their own async mirror, so no rank is left waiting in a collective."""
+    from gossip_protocol_amd._lib import GspError
+    from gossip_protocol_amd.scale import nccl_unique_id
+    monkeypatch.setenv("GSP_TEST_MAX_SEGMENT", "2")
+    kw = dict(fanout=8, max_ticks=10)
+    if form == "rows3":
+        kw.update(group=3, layout="rows")
+    elif form == "columns2":
+        kw.update(group=2)
+    else:
+        kw.update(rank=0, world=1, nccl_id=nccl_unique_id(),
+                  layout="rows" if form == "rank_rows" else "columns")
+    with ScaleEngine(2048, **kw) as eng:
+        eng.step(1)                      # tick 1: ~8 messages per receiver > 2
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.sync()
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.step(1)
+            eng.sync()
+        with pytest.raises(GspError, match="at tick 1"):
+            eng.digest(1)
