@@ -256,8 +256,8 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
-        GSP_HIP(sh.prof.alloc(64 * gsp::kPvProfPhases));
-        GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * gsp::kPvProfPhases * 8, st));
+        GSP_HIP(sh.prof.alloc(64 * 8 * gsp::kPvProfPhases));
+        GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * 8 * gsp::kPvProfPhases * 8, st));
     }
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * 8, st));
     GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
@@ -472,16 +472,23 @@ int gsp_pview_destroy(gsp_pview *s) {
     }
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
     for (PvShard &sh : s->local) {
-        if (sh.prof.p) {   // GSP_PV_PROFILE diagnostics: cycles per phase, sampled rows
-            std::vector<unsigned long long> h(64 * gsp::kPvProfPhases);
+        if (sh.prof.p) {   // GSP_PV_PROFILE diagnostics: cycles per phase of sampled rows, by k
+            constexpr int P = gsp::kPvProfPhases;
+            std::vector<unsigned long long> h(64 * 8 * P);
             if (hipMemcpy(h.data(), sh.prof.p, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-                unsigned long long ph[gsp::kPvProfPhases] = {0}, tot = 0;
-                for (size_t i = 0; i < h.size(); ++i) ph[i % gsp::kPvProfPhases] += h[i];
-                for (unsigned long long v : ph) tot += v;
-                std::fprintf(stderr, "pview phases (shard %d, %% of sampled cycles):", sh.g);
-                for (int i = 0; i < gsp::kPvProfPhases; ++i)
-                    std::fprintf(stderr, " p%d=%.1f", i, tot ? 100.0 * double(ph[i]) / double(tot) : 0.0);
-                std::fprintf(stderr, " total=%llu\n", tot);
+                unsigned long long ph[8][P] = {{0}};
+                for (size_t i = 0; i < h.size(); ++i) ph[(i / P) % 8][i % P] += h[i];
+                for (int k = 0; k < 8; ++k) {
+                    const unsigned long long rows = ph[k][P - 1];
+                    if (!rows) continue;
+                    unsigned long long tot = 0;
+                    for (int i = 0; i < P - 1; ++i) tot += ph[k][i];
+                    std::fprintf(stderr, "pview phases (shard %d) k=%d rows=%llu cycles/row=%.0f:", sh.g, k,
+                                 rows, double(tot) / double(rows));
+                    for (int i = 0; i < P - 1; ++i)
+                        if (ph[k][i]) std::fprintf(stderr, " p%d=%.0f", i, double(ph[k][i]) / double(rows));
+                    std::fprintf(stderr, "\n");
+                }
             }
         }
         sh.release();

@@ -203,13 +203,15 @@ __device__ inline int32_t lds_half(const Sh &sh, const void *p) {
 }
 
 // Diagnostics (GSP_PV_PROFILE=1): thread 0 of every 16th row adds the cycles since the last
-// mark to prof[slot][phase]; a scalar branch on a kernel argument when off.
+// mark to prof[slot][k][phase] (phase kPvProfPhases - 1 counts the sampled rows); a scalar
+// branch on a kernel argument when off.
 struct PvMark {
     unsigned long long *out = nullptr;
     uint64_t last = 0;
-    __device__ __forceinline__ void init(unsigned long long *prof) {
+    __device__ __forceinline__ void init(unsigned long long *prof, int32_t k) {
         if (prof && threadIdx.x == 0 && (blockIdx.x & 15u) == 0) {
-            out = prof + (blockIdx.x >> 4 & 63u) * kPvProfPhases;
+            out = prof + ((blockIdx.x >> 4 & 63u) * 8 + uint32_t(k & 7)) * kPvProfPhases;
+            atomicAdd(out + kPvProfPhases - 1, 1ull);
             last = clock64();
         }
     }
@@ -415,6 +417,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         }
         pv_sync<NT>();
         cur ^= 1;
+        pm.mark(s == kSlots ? 12 : s == 2 * kSlots ? 13 : 14);
     }
     const int32_t beg = tid * Q;                               // the fold's Q keys per lane
     const uint32_t *C = sh.keys[cur];
@@ -678,8 +681,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             nt += is_tie ? 1u : 0u;
             nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
         });
+        pm.mark(9);
         uint32_t sums = 0;
         const uint32_t ex = block_scan<NT>(nt | (nk << 16), &sums, scan_buf + 4);
+        pm.mark(10);
         uint32_t tie_before = ex & 0xFFFFu;
         const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
@@ -712,6 +717,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         ro.ids_off = lds_word(sh, Wid);
         ro.vals_off = lds_half(sh, Wval);
         ro.len = V;
+        pm.mark(11);
     }
     ro.joins = joins;
     ro.removes = removes;
@@ -808,10 +814,10 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
         return;
     }
     PvMark pm;
-    pm.init(a.prof);
     RowOut ro{};
     const int32_t info = __builtin_amdgcn_readfirstlane(info_v);
     const int32_t k = info & 7, k_all = info >> 3;
+    pm.init(a.prof, k);
     // a JOINREP (sender kJoinRepSrc) sorts first; its sender event is node 0's
     const bool jrep = (kExt & kExtPol) && k > 0 && __builtin_amdgcn_readfirstlane(my_src) == kJoinRepSrc;
     uint32_t ssrc[kPvMaxInbox];
@@ -924,15 +930,9 @@ __global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTi
 }
 
 // The split kernels' k ranges, in launch order (launch_pview_tick).
-#ifdef GSP_PV_NT64
-constexpr int kPvRanges = 5;
-__device__ __forceinline__ int32_t pv_range_lo(int32_t j) { return j == 0 ? 6 : j == 1 ? 5 : j == 2 ? 4 : j == 3 ? 2 : 0; }
-__device__ __forceinline__ int32_t pv_range_hi(int32_t j) { return j == 0 ? 7 : j == 1 ? 5 : j == 2 ? 4 : j == 3 ? 3 : 1; }
-#else
 constexpr int kPvRanges = 4;
 __device__ __forceinline__ int32_t pv_range_lo(int32_t j) { return j == 0 ? 6 : j == 1 ? 5 : j == 2 ? 4 : 0; }
 __device__ __forceinline__ int32_t pv_range_hi(int32_t j) { return j == 0 ? 7 : j == 1 ? 5 : j == 2 ? 4 : 3; }
-#endif
 
 // The rows of every split range at or past that kernel's grid (a.split_grid[j]): the grids the
 // host predicted were too small for this tick's buckets.  A fixed grid; each workgroup runs
@@ -1200,7 +1200,11 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         // (the heavy rows first).  Grids: the exact bucket sizes, read back synchronously
         // (a.kcount_host, GSP_PV_SPLITSYNC=1), or -- by default, no host wait -- predicted from
         // the last counts the host has seen (a.kcount_seen, copied back asynchronously each
-        // tick; 6 % + 256 of margin), every row past a grid run by the overflow kernel.
+        // tick), with 25 % + 1024 of margin: the mean k of config 5 falls from ~2.6 to ~1.6 over
+        // ticks 6-25 while the host predicts every one of them from tick 5, so the k <= 3 bucket
+        // grows past a tight margin (6 % + 256: +3.5 % tick time, rows run by the overflow
+        // kernel); a workgroup past its bucket exits after reading the counts.  Every row past a
+        // grid is run by the overflow kernel.
         PviewTickArgs b = a;
         int32_t c[8];
         const bool exact = a.kcount_host != nullptr;
@@ -1221,35 +1225,22 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
                 }
                 g += c[q];
             }
-            if (!exact) g += g / 16 + 256;
+            if (!exact) g += g / 4 + 1024;
             if (!exact && a.test_grid_cap > 0 && g > a.test_grid_cap) g = a.test_grid_cap;
             return int32_t(g < a.rows ? g : a.rows);
         };
         b.split_grid[0] = grid(6, 7);
         b.split_grid[1] = grid(5, 5);
         b.split_grid[2] = grid(4, 4);
-#ifdef GSP_PV_NT64
-        b.split_grid[3] = grid(2, 3);
-        b.split_grid[4] = grid(0, 1);
-#else
         b.split_grid[3] = grid(0, 3);
-#endif
         const int32_t cus = a.cus > 0 ? a.cus : 256;
         const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
-#ifdef GSP_PV_NT64   // k = 2, 3 as 128-lane rows, k = 0, 1 as one-wave rows in 5 KB (32 per CU)
-#define GSP_PV_SMALL_ROWS(E)                                                                              \
-        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 2, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b); \
-        if (b.split_grid[4]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 64, 0, 1>), dim3(b.split_grid[4]), dim3(64), 0, st, b);
-#else
-#define GSP_PV_SMALL_ROWS(E)                                                                              \
-        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
-#endif
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
     do {                                                                                                  \
         if (b.split_grid[0]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(b.split_grid[0]), dim3(256), 0, st, b); \
         if (b.split_grid[1]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b); \
         if (b.split_grid[2]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b); \
-        GSP_PV_SMALL_ROWS(E)                                                                              \
+        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b); \
         if (!exact) hipLaunchKernelGGL((pview_tick_overflow_kernel<E>), dim3(gov), dim3(kPvBlock), 0, st, b); \
     } while (0)
 #ifdef GSP_PV_EXP_PLAIN_ONLY   // experiments: the plain protocol's kernels only (fast builds)
@@ -1264,7 +1255,6 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         }
 #endif
 #undef GSP_PV_SPLIT_LAUNCH
-#undef GSP_PV_SMALL_ROWS
         launch_send_and_digest(b, st);
         return hipGetLastError();
     }

@@ -63,11 +63,11 @@ struct PviewTickArgs {
     const int32_t *kcount_seen;  // host, pinned [8]: the last bucket sizes copied back (any
                                  // value is safe: it only sizes grids), or null
     int32_t cus;                 // compute units of the device (overflow kernel grid)
-    int32_t split_grid[5];       // set by launch_pview_tick: the split kernels' grids
+    int32_t split_grid[4];       // set by launch_pview_tick: the split kernels' grids
     int32_t test_grid_cap;       // tests only (GSP_TEST_PV_GRID_CAP): cap on every predicted
                                  // split grid, so the overflow kernel runs most rows (0: none)
 };
-constexpr int kPvProfPhases = 10;
+constexpr int kPvProfPhases = 16;   // per (slot, k): phases 0..14, rows sampled
 
 struct PviewReceiptArgs {
     const int32_t *off;          // [rows + 1] receiver CSR
