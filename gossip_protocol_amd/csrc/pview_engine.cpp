@@ -37,7 +37,7 @@ namespace {
 struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
-    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, deg, off, fill, csr_src, err,
+    gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, out_pos, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok;
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
@@ -46,7 +46,7 @@ struct PvShard {
 
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
-        for (auto *b : {&own_hb, &fail_tick, &out_dst, &deg, &off, &fill, &csr_src, &err,
+        for (auto *b : {&own_hb, &fail_tick, &out_dst, &out_pos, &deg, &off, &fill, &csr_src, &err,
                         &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order, &start_tick, &ping,
                         &joiners, &join_ok})
             b->release();
@@ -74,10 +74,15 @@ struct gsp_pview {
     bool timing = true;
     int32_t split = 1;           // GSP_PV_SPLIT=0: every row in the one 256-lane kernel; else
                                  // rows bucketed by k into four kernels (pview_kernels.hip)
+    bool pos_scatter = false;    // one shard, no join schedule: the receiver CSR is scattered from
+                                 // the positions the send kernel's deg atomics returned (the
+                                 // JOINREP append and the row exchange keep the fill counters)
     bool split_sync = false;     // GSP_PV_SPLITSYNC=1: exact split grids from the counts read
                                  // back, one stream sync per tick; default: persistent grids, no
                                  // host wait (gsp_pview_step queues its ticks back to back)
     int32_t cus = 0;             // compute units (overflow kernel grid)
+    int32_t grid_margin = 100;   // GSP_PV_GRID_MARGIN: predicted split grids, percent over the
+                                 // last bucket sizes seen
     int32_t test_grid_cap = 0;   // GSP_TEST_PV_GRID_CAP (tests: force the overflow kernel)
     int32_t *h_kcount = nullptr; // pinned [8] for split_sync
     int32_t *h_kseen = nullptr;  // pinned [local][8]: each shard's bucket sizes, copied back
@@ -137,6 +142,7 @@ struct gsp_pview {
         a.rc_src = sh.rc_src.p;
         a.rc_slot = sh.rc_slot.p;
         a.out_dst = sh.out_dst.p;
+        a.out_pos = sh.out_pos.p;
         a.rowdig = sh.rowdig.p;
         a.deg = sh.deg.p;
         a.dig = sh.dig.p + size_t(t) * gsp::kPvDigSlots * gsp::kPvFields;
@@ -149,6 +155,7 @@ struct gsp_pview {
         a.kcount_host = h_kcount;
         a.kcount_seen = h_kseen ? h_kseen + 8 * (&sh - local.data()) : nullptr;
         a.cus = cus;
+        a.grid_margin = grid_margin;
         a.test_grid_cap = test_grid_cap;
         a.ev = sh.ev.args();
         return a;
@@ -218,6 +225,7 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     GSP_HIP(sh.own_hb.alloc(rows));
     GSP_HIP(sh.fail_tick.alloc(size_t(n)));
     GSP_HIP(sh.out_dst.alloc(rows * F));
+    if (s->pos_scatter) GSP_HIP(sh.out_pos.alloc(rows * F));
     GSP_HIP(sh.deg.alloc(size_t(n)));
     GSP_HIP(sh.off.alloc(rows + 1));
     GSP_HIP(sh.fill.alloc(rows));
@@ -384,6 +392,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     if (const char *ss = std::getenv("GSP_PV_SPLITSYNC")) s->split_sync = std::atoi(ss) != 0;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
     if (const char *gc = std::getenv("GSP_TEST_PV_GRID_CAP")) s->test_grid_cap = std::max(0, std::atoi(gc));
+    if (const char *gm = std::getenv("GSP_PV_GRID_MARGIN")) s->grid_margin = std::max(0, std::min(1000, std::atoi(gm)));
     if (s->split_sync && s->split && s->sort_rows)
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
     GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -394,6 +403,8 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
+    s->pos_scatter = !s->rowmode && !s->joins;
+    if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
     int32_t max_rows = 0;
     for (int32_t g = 0; g < shards; ++g)
@@ -526,9 +537,15 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         } else {
             PvShard &sh = s->local[0];
             GSP_HIP(gsp::launch_exclusive_scan(sh.deg.p, sh.off.p, n, sh.tile_sum.p, s->st));
-            GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
-            GSP_HIP(gsp::launch_scatter(sh.out_dst.p, int64_t(n) * s->p.fanout, s->p.fanout, 0,
-                                        sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
+            if (s->pos_scatter) {     // each message's slot in its receiver's segment came back
+                                      // from the send kernel's deg atomic: no atomics here
+                GSP_HIP(gsp::launch_pview_scatter(sh.out_dst.p, sh.out_pos.p, int64_t(n) * s->p.fanout,
+                                                  s->p.fanout, sh.off.p, sh.csr_src.p, s->st));
+            } else {
+                GSP_HIP(hipMemsetAsync(sh.fill.p, 0, size_t(n) * 4, s->st));
+                GSP_HIP(gsp::launch_scatter(sh.out_dst.p, int64_t(n) * s->p.fanout, s->p.fanout, 0,
+                                            sh.off.p, sh.fill.p, sh.csr_src.p, s->st));
+            }
             GSP_HIP(hipMemsetAsync(sh.deg.p, 0, size_t(n) * 4, s->st));
         }
         if (int rc = pv_join_scatter(s, t)) return rc;

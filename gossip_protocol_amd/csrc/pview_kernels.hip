@@ -28,6 +28,10 @@
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include <algorithm>
 
+#ifndef GSP_PV_K67_WAVES      // waves per SIMD the k = 6, 7 kernel is compiled for (A/B experiments)
+#define GSP_PV_K67_WAVES 8
+#endif
+
 #include "join_kernels.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
@@ -1105,7 +1109,10 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
             if (int32_t(dr % 100u) < a.drop_pct) { d = -1; dropped++; }
         }
         od[kk] = d;
-        if (d >= 0) atomicAdd(&a.deg[d], 1);
+        if (d >= 0) {
+            const int32_t pos = atomicAdd(&a.deg[d], 1);
+            if (a.out_pos) a.out_pos[int64_t(lr) * F + kk] = pos;
+        }
     }
     if (a.swim > 0) {          // this tick's probe target: one more rank over the same order
         int32_t p = -1;
@@ -1153,6 +1160,18 @@ __global__ void __launch_bounds__(256) pview_digest_kernel(const unsigned long l
     }
 }
 
+// Receiver CSR of one shard without atomics: message i of sender row i / F goes to slot
+// out_pos[i] of its receiver's segment (MP1Node's queue order is not kept by any scatter: the
+// receipt kernel sorts each segment's senders).
+__global__ void pview_scatter_kernel(const int32_t *out_dst, const int32_t *out_pos, int64_t slots,
+                                     int32_t fanout, const int32_t *off, int32_t *csr_src) {
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < slots;
+         i += int64_t(gridDim.x) * blockDim.x) {
+        const int32_t d = out_dst[i];
+        if (d >= 0) csr_src[off[d] + out_pos[i]] = int32_t(i / fanout);
+    }
+}
+
 bool pv_args_ok(const PviewTickArgs &a) {
     return a.view >= 1 && a.view <= kPvMaxView && a.inbox >= 1 && a.inbox <= kPvMaxInbox &&
            a.fanout >= 1 && a.fanout <= 16 && a.n < (1 << 21) && a.rows >= 0;
@@ -1180,6 +1199,15 @@ hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st) {
     return hipGetLastError();
 }
 
+hipError_t launch_pview_scatter(const int32_t *out_dst, const int32_t *out_pos, int64_t slots,
+                                int32_t fanout, const int32_t *off, int32_t *csr_src, hipStream_t st) {
+    if (slots <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((slots + 255) / 256, 8192);
+    hipLaunchKernelGGL(pview_scatter_kernel, dim3(unsigned(blocks)), dim3(256), 0, st, out_dst, out_pos,
+                       slots, fanout, off, csr_src);
+    return hipGetLastError();
+}
+
 hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st) {
     if (a.inbox < 1 || a.inbox > kPvMaxInbox || a.rows < 0) return hipErrorInvalidValue;
     if (a.rows == 0) return hipSuccess;
@@ -1200,11 +1228,11 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         // (the heavy rows first).  Grids: the exact bucket sizes, read back synchronously
         // (a.kcount_host, GSP_PV_SPLITSYNC=1), or -- by default, no host wait -- predicted from
         // the last counts the host has seen (a.kcount_seen, copied back asynchronously each
-        // tick), with 25 % + 1024 of margin: the mean k of config 5 falls from ~2.6 to ~1.6 over
-        // ticks 6-25 while the host predicts every one of them from tick 5, so the k <= 3 bucket
-        // grows past a tight margin (6 % + 256: +3.5 % tick time, rows run by the overflow
-        // kernel); a workgroup past its bucket exits after reading the counts.  Every row past a
-        // grid is run by the overflow kernel.
+        // tick), with a.grid_margin % + 1024 rows of margin: a host that queues many ticks
+        // predicts all of them from one tick's counts while the buckets drift (config 5, ticks
+        // 6-25 from tick 5: the k = 6, 7 bucket grows by a third as in-degrees skew); a
+        // workgroup past its bucket exits after reading the counts.  Every row past a grid is
+        // run by the overflow kernel.
         PviewTickArgs b = a;
         int32_t c[8];
         const bool exact = a.kcount_host != nullptr;
@@ -1225,7 +1253,7 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
                 }
                 g += c[q];
             }
-            if (!exact) g += g / 4 + 1024;
+            if (!exact) g += g * a.grid_margin / 100 + 1024;
             if (!exact && a.test_grid_cap > 0 && g > a.test_grid_cap) g = a.test_grid_cap;
             return int32_t(g < a.rows ? g : a.rows);
         };
@@ -1237,7 +1265,7 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
     do {                                                                                                  \
-        if (b.split_grid[0]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7>), dim3(b.split_grid[0]), dim3(256), 0, st, b); \
+        if (b.split_grid[0]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, GSP_PV_K67_WAVES>), dim3(b.split_grid[0]), dim3(256), 0, st, b); \
         if (b.split_grid[1]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b); \
         if (b.split_grid[2]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b); \
         if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b); \

@@ -45,6 +45,8 @@ struct PviewTickArgs {
     const int32_t *rc_src;       // [rows][8] the k smallest senders, ascending
     const int32_t *rc_slot;      // [rows][8] their rows: >= 0 local, < 0 remote (-slot - 1)
     int32_t *out_dst;            // [rows * fanout]
+    int32_t *out_pos;            // [rows * fanout]: each message's slot in its receiver's CSR
+                                 // segment (the send kernel's deg atomic), or null
     int32_t *deg;                // [n]
     unsigned long long *rowdig;  // [rows][4][4] per-row digest records of this tick
     unsigned long long *dig;     // [kPvDigSlots][kPvFields] of this tick
@@ -64,6 +66,8 @@ struct PviewTickArgs {
                                  // value is safe: it only sizes grids), or null
     int32_t cus;                 // compute units of the device (overflow kernel grid)
     int32_t split_grid[4];       // set by launch_pview_tick: the split kernels' grids
+    int32_t grid_margin;         // predicted grids: last counts seen * (100 + grid_margin) / 100
+                                 // + 1024 (GSP_PV_GRID_MARGIN, percent)
     int32_t test_grid_cap;       // tests only (GSP_TEST_PV_GRID_CAP): cap on every predicted
                                  // split grid, so the overflow kernel runs most rows (0: none)
 };
@@ -83,5 +87,8 @@ hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st);
 hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st);
 // tick kernel, then the send kernel (peers, drops) and the digest reduction
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st);
+// receiver CSR of one shard from the send kernel's positions: csr_src[off[d] + pos] = sender
+hipError_t launch_pview_scatter(const int32_t *out_dst, const int32_t *out_pos, int64_t slots,
+                                int32_t fanout, const int32_t *off, int32_t *csr_src, hipStream_t st);
 
 }  // namespace gsp
