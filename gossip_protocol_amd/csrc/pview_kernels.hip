@@ -27,10 +27,20 @@
 //      pview_digest_kernel.
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include <algorithm>
+#include <type_traits>
 
 #ifndef GSP_PV_K67_WAVES      // waves per SIMD the k = 6, 7 kernel is compiled for (A/B experiments)
 #define GSP_PV_K67_WAVES 8
 #endif
+#ifndef GSP_PV_K4_WAVES       // waves per SIMD of the in-place k = 4 / k = 5 kernels (14 / 12 rows
+#define GSP_PV_K4_WAVES 7     // per CU; 8 / 7 spill 24 / 20 B)
+#endif
+#ifndef GSP_PV_K5_WAVES
+#define GSP_PV_K5_WAVES 6
+#endif
+#ifndef GSP_PV_IP             // in-place rows (PvSharedIP), a bit mask: 1 k = 6, 7 as 128-lane in-place
+#define GSP_PV_IP 2           // rows (A/B +1.9 %), 2 k = 4, 5 in place (the default: -1.3 %), 4 k <= 3
+#endif                        // in place (±0)
 
 #include "join_kernels.hpp"
 #include "philox.hpp"
@@ -185,21 +195,57 @@ __device__ inline void lds_load(const uint32_t *p, uint32_t (&v)[N]) {
 // of keys[cur ^ 1], the kept values follow the kept ids at word 256 of keys[cur], the exact
 // hb histogram spans both halves (one wave: the bins are read before it is zeroed), and
 // block scans need no buffer.
+// Accessors (both layouts): kb(i) merge buffer i, bins / scanbuf the eviction histogram and
+// block-scan words after the tree, pre() block-scan words before it, uids the survivor ids
+// when nothing is evicted, wids / wvals the kept view, hist the exact hb histogram.
 template <int kKeys>
 struct alignas(16) PvShared {
     static_assert(kKeys == 512 || (kKeys >= 1024 && kKeys <= 2048 && kKeys % 256 == 0),
                   "2 (one-wave rows) or 4 to 8 sources of 256 keys");
+    static constexpr bool kInPlace = false;
     static constexpr int kHist = kKeys == 512 ? 0 : kKeys - 1024,
                          kScan = kKeys == 512 ? 0 : kKeys > 1024 ? kKeys - 8 : 504,
                          kWValWord = kKeys == 512 ? 256 : 512, kBinWord = kKeys == 512 ? 0 : 512;
     uint32_t keys[2][kKeys];             // merge ping-pong; then the regions above
     uint16_t vals[kKeys];                // values by (source, slot); then survivor values
     __device__ uint32_t *hist(int cur) { return kKeys == 512 ? &keys[0][0] : keys[cur] + kHist; }
+    __device__ uint32_t *kb(int i) { return keys[i]; }
+    __device__ const uint32_t *base() const { return &keys[0][0]; }
+    __device__ uint32_t *bins(int cur) { return keys[cur ^ 1] + kBinWord; }
+    __device__ uint32_t *scanbuf(int cur) { return keys[cur ^ 1] + kScan; }
+    __device__ uint32_t *pre() { return keys[1]; }
+    __device__ uint32_t *uids(int cur) { return keys[cur ^ 1]; }
+    __device__ uint32_t *wids(int cur) { return keys[cur]; }
+    __device__ uint16_t *wvals(int cur) { return reinterpret_cast<uint16_t *>(keys[cur] + kWValWord); }
+};
+
+// One merge buffer, merged in place (a tree level reads its inputs into registers, then a
+// barrier, then writes): 4 B + 2 B per key + 2 KB of bins and scan words -- 8.3 / 9.8 / 11.3 /
+// 14.4 KB for 4 / 5 / 6 / 8 sources instead of 10 / 12.5 / 15 / 20 KB, so the rows merging 4
+// or more messages fit more rows per CU, for one more barrier per tree level.  After the fold
+// the key buffer holds the kept view (ids [0, 256), values at word 512) and, before them, the
+// exact hb histogram (1024 words at kKeys - 1024).
+template <int kKeys>
+struct alignas(16) PvSharedIP {
+    static_assert(kKeys >= 1024 && kKeys <= 2048 && kKeys % 256 == 0, "4 to 8 sources of 256 keys");
+    static constexpr bool kInPlace = true;
+    uint32_t keys[kKeys];
+    uint16_t vals[kKeys];
+    uint32_t aux[512 + 16];              // eviction bins (1024 u16), then 16 block-scan words
+    __device__ uint32_t *hist(int) { return keys + (kKeys - 1024); }
+    __device__ uint32_t *kb(int) { return keys; }
+    __device__ const uint32_t *base() const { return keys; }
+    __device__ uint32_t *bins(int) { return aux; }
+    __device__ uint32_t *scanbuf(int) { return aux + 512; }
+    __device__ uint32_t *pre() { return aux; }
+    __device__ uint32_t *uids(int) { return keys; }
+    __device__ uint32_t *wids(int) { return keys; }
+    __device__ uint16_t *wvals(int) { return reinterpret_cast<uint16_t *>(keys + 512); }
 };
 
 template <class Sh>
 __device__ inline int32_t lds_word(const Sh &sh, const uint32_t *p) {
-    return int32_t(p - &sh.keys[0][0]);
+    return int32_t(p - sh.base());
 }
 template <class Sh>
 __device__ inline int32_t lds_half(const Sh &sh, const void *p) {
@@ -321,7 +367,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
 #pragma unroll
         for (int i = 0; i < SL; ++i) gl += ent[1][i] != kPvEmpty ? 1u : 0u;
         uint32_t cnt0 = 0;
-        uint32_t rank = block_scan<NT>(gl, &cnt0, sh.keys[1]);   // keys[1] is free here
+        uint32_t rank = block_scan<NT>(gl, &cnt0, sh.pre());     // free before the tree
         const int32_t B = a.intro_list < int32_t(cnt0) ? a.intro_list : int32_t(cnt0);
         uint64_t cm[4];
         pv_intro_mask(a.seed, t - 1u, uint32_t(r), int32_t(cnt0), B, cm);
@@ -347,7 +393,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
 #pragma unroll
             for (int i = 0; i < SL; ++i) cl += ent[m][i] != kPvEmpty ? 1u : 0u;
             uint32_t cnt = 0;
-            uint32_t pos = block_scan<NT>(cl, &cnt, sh.keys[1] + 16 + 8 * (m & 1));
+            uint32_t pos = block_scan<NT>(cl, &cnt, sh.pre() + 16 + 8 * (m & 1));
 #pragma unroll
             for (int i = 0; i < SL; ++i) {
                 const bool ok = ent[m][i] != kPvEmpty;
@@ -365,12 +411,12 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             const int32_t slot = tid * SL + i;
             const bool ok = ent[m][i] != kPvEmpty;
             merged += (m >= 1 && ok) ? 1u : 0u;
-            if ((kExt & kExtPol) && ((kpad >> (m * SL + i)) & 1u)) sh.keys[0][m * kSlots + slot] = kKeyMax;
+            if ((kExt & kExtPol) && ((kpad >> (m * SL + i)) & 1u)) sh.kb(0)[m * kSlots + slot] = kKeyMax;
             if (!(kExt & kExtPol) || kpos[m][i] >= 0)
-                sh.keys[0][m * kSlots + kpos[m][i]] =
+                sh.kb(0)[m * kSlots + kpos[m][i]] =
                     ok ? (uint32_t(ent[m][i] >> 32) << 11) | (uint32_t(m) << 8) | uint32_t(slot) : kKeyMax;
             sh.vals[m * kSlots + slot] = uint16_t(ent[m][i]);
-            if (m > k) sh.keys[1][m * kSlots + slot] = kKeyMax;     // padding for the ping-pong
+            if (!Sh::kInPlace && m > k) sh.kb(1)[m * kSlots + slot] = kKeyMax;   // padding for the ping-pong
         }
     }
     pv_sync<NT>();
@@ -387,9 +433,10 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     int cur = 0;
 #pragma unroll
     for (int s = kSlots; s < P; s <<= 1) {
-        if (begt < Pe) {
-            const uint32_t *X = sh.keys[cur];
-            uint32_t *Y = sh.keys[cur ^ 1];
+        uint32_t outk[Qt];
+        const bool act = begt < Pe;
+        if (act) {
+            const uint32_t *X = sh.kb(cur);
             const int32_t b = begt / (2 * s), o = begt - b * 2 * s;
             const uint32_t *A = X + b * 2 * s, *B = A + s;
             int32_t sa = s, sb = s;
@@ -404,7 +451,6 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
                 if (A[mid] < B[o - mid - 1]) lo = mid + 1; else hi = mid;
             }
             int32_t i = lo, j = o - lo;
-            uint32_t outk[Qt];
             uint32_t va = i < sa ? A[i] : kKeyMax, vb = j < sb ? B[j] : kKeyMax;
 #pragma unroll
             for (int e = 0; e < Qt; ++e) {
@@ -417,19 +463,23 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
                 va = ta ? nv : va;
                 vb = ta ? vb : nv;
             }
-            lds_store<Qt>(Y + begt, outk);
+            if constexpr (!Sh::kInPlace) lds_store<Qt>(sh.kb(cur ^ 1) + begt, outk);
+        }
+        if constexpr (Sh::kInPlace) {            // one buffer: every input of the level is read
+            pv_sync<NT>();                       // before any output is written over it
+            if (act) lds_store<Qt>(sh.kb(0) + begt, outk);
         }
         pv_sync<NT>();
-        cur ^= 1;
+        if constexpr (!Sh::kInPlace) cur ^= 1;
         pm.mark(s == kSlots ? 12 : s == 2 * kSlots ? 13 : 14);
     }
     const int32_t beg = tid * Q;                               // the fold's Q keys per lane
-    const uint32_t *C = sh.keys[cur];
-    // keys[cur ^ 1] (the last level's source) is dead after the tree: it holds the eviction
-    // histogram over (age, hb) bins (1024 u16 counters at words [512, 1024)) and the scan
-    // buffers (8 words at Sh::kScan)
-    uint32_t *const bins = sh.keys[cur ^ 1] + Sh::kBinWord;
-    uint32_t *const scan_buf = sh.keys[cur ^ 1] + Sh::kScan;
+    const uint32_t *C = sh.kb(cur);
+    // the eviction histogram over (age, hb) bins (1024 u16 counters) and the block-scan words:
+    // ping-pong layout, in keys[cur ^ 1] (the last level's source, dead after the tree) at
+    // words [512, 1024) and Sh::kScan; in-place layout, in their own words
+    uint32_t *const bins = sh.bins(cur);
+    uint32_t *const scan_buf = sh.scanbuf(cur);
 #pragma unroll
     for (int i = tid; i < 256; i += NT) reinterpret_cast<uint2 *>(bins)[i] = make_uint2(0u, 0u);
 
@@ -586,7 +636,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     const uint32_t base = block_scan<NT>(nloc, &total, scan_buf);
     const bool evict = int32_t(total) > V;
     if (!evict) {                                              // the survivors are the view
-        uint32_t *Uid = sh.keys[cur ^ 1];
+        uint32_t *Uid = sh.uids(cur);
         uint16_t *Uval = sh.vals;                              // the gathered values are dead
         uint32_t w = base;
         for_each([&](uint32_t v, uint32_t x, uint32_t) {
@@ -692,8 +742,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         uint32_t tie_before = ex & 0xFFFFu;
         const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
-        uint32_t *Wid = sh.keys[cur];
-        uint16_t *Wval = reinterpret_cast<uint16_t *>(sh.keys[cur] + Sh::kWValWord);
+        uint32_t *Wid = sh.wids(cur);
+        uint16_t *Wval = sh.wvals(cur);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
         const bool ev_on = (kExt & kExtEv) && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
         if (ev_on) {
@@ -742,7 +792,7 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_
     const int32_t tid = pv_tid<NT>(), lane = tid & 63, wave = tid >> 6;
     const int32_t V = a.view, len = ro.len;
     const uint32_t t = uint32_t(a.tick);
-    const uint32_t *ids = &sh.keys[0][0] + ro.ids_off;
+    const uint32_t *ids = sh.base() + ro.ids_off;
     const uint16_t *vals = reinterpret_cast<const uint16_t *>(&sh) + ro.vals_off;
     uint64_t *out = a.cur + int64_t(lr) * V;
     for (int32_t i = tid; i < V; i += NT)
@@ -921,9 +971,10 @@ __global__ void __launch_bounds__(kPvBlock, 8) pview_tick_kernel(PviewTickArgs a
 // rows in 20 KB.  Workgroup b runs the b-th row of its buckets' k-descending order; rows at
 // or past the grid belong to pview_tick_overflow_kernel (the grid is either the exact bucket
 // size, read back by the host, or the host's prediction from the last counts it has seen).
-template <int kExt, int NT, int kQlo, int kQhi, int kMinWaves = 8>
+template <int kExt, int NT, int kQlo, int kQhi, int kMinWaves = 8, bool kIP = false>
 __global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTickArgs a) {
-    __shared__ PvShared<NT == 64 ? 512 : kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots> sh;
+    constexpr int kKeys = NT == 64 ? 512 : kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots;
+    __shared__ std::conditional_t<kIP, PvSharedIP<kKeys>, PvShared<kKeys>> sh;
     static_assert(NT != 64 || kQhi <= 1, "one-wave rows hold at most 2 sources");
     int32_t total = 0;
 #pragma unroll
@@ -1263,12 +1314,29 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         b.split_grid[3] = grid(0, 3);
         const int32_t cus = a.cus > 0 ? a.cus : 256;
         const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
+#if GSP_PV_IP & 1
+#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 6, 7, 5, true>), dim3(b.split_grid[0]), dim3(128), 0, st, b);
+#else
+#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, GSP_PV_K67_WAVES>), dim3(b.split_grid[0]), dim3(256), 0, st, b);
+#endif
+#if GSP_PV_IP & 2
+#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, GSP_PV_K5_WAVES, true>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
+#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, GSP_PV_K4_WAVES, true>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
+#else
+#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
+#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
+#endif
+#if GSP_PV_IP & 4
+#define GSP_PV_K03(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3, 8, true>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
+#else
+#define GSP_PV_K03(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
+#endif
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
     do {                                                                                                  \
-        if (b.split_grid[0]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, GSP_PV_K67_WAVES>), dim3(b.split_grid[0]), dim3(256), 0, st, b); \
-        if (b.split_grid[1]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b); \
-        if (b.split_grid[2]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b); \
-        if (b.split_grid[3]) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b); \
+        if (b.split_grid[0]) GSP_PV_K67(E)                                                                \
+        if (b.split_grid[1]) GSP_PV_K5(E)                                                                 \
+        if (b.split_grid[2]) GSP_PV_K4(E)                                                                 \
+        if (b.split_grid[3]) GSP_PV_K03(E)                                                                \
         if (!exact) hipLaunchKernelGGL((pview_tick_overflow_kernel<E>), dim3(gov), dim3(kPvBlock), 0, st, b); \
     } while (0)
 #ifdef GSP_PV_EXP_PLAIN_ONLY   // experiments: the plain protocol's kernels only (fast builds)
@@ -1283,6 +1351,10 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         }
 #endif
 #undef GSP_PV_SPLIT_LAUNCH
+#undef GSP_PV_K67
+#undef GSP_PV_K5
+#undef GSP_PV_K4
+#undef GSP_PV_K03
         launch_send_and_digest(b, st);
         return hipGetLastError();
     }
