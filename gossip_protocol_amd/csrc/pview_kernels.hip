@@ -281,6 +281,7 @@ struct RowOut {
     int32_t len;
     uint32_t joins, removes, evicts, merged;
     uint64_t hsum;
+    bool written;                 // the view is already in HBM (pv_own_only)
 };
 
 // The bounded introducer list (block-uniform): bit q of m = rank q of node 0's gossiped members
@@ -795,9 +796,10 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_
     const uint32_t *ids = sh.base() + ro.ids_off;
     const uint16_t *vals = reinterpret_cast<const uint16_t *>(&sh) + ro.vals_off;
     uint64_t *out = a.cur + int64_t(lr) * V;
-    for (int32_t i = tid; i < V; i += NT)
-        __builtin_nontemporal_store(
-            i < len ? (uint64_t(ids[i]) << 32) | uint64_t(vals[i]) : kPvEmpty, out + i);
+    if (!ro.written)
+        for (int32_t i = tid; i < V; i += NT)
+            __builtin_nontemporal_store(
+                i < len ? (uint64_t(ids[i]) << 32) | uint64_t(vals[i]) : kPvEmpty, out + i);
     if (init) {
         if (tid == 0) a.len_cur[lr] = len;
         return;
@@ -829,6 +831,45 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_
             z[0] = z[1] = make_ulonglong2(0ull, 0ull);
         }
     }
+}
+
+// A row that merges no message (k = 0, ~30 % of config 5's rows), plain protocol: its view is
+// its own view minus the entries TREMOVE drops (MP1Node.cpp:339-348) -- no union, no fold
+// state, nothing to evict -- so the kept entries go from registers straight to HBM in id order
+// (one block scan for their positions), byte for byte the entries they were.
+template <int NT, class Sh>
+__device__ __forceinline__ void pv_own_only(const PviewTickArgs &a, Sh &sh, int32_t r, int32_t lr,
+                                            const uint64_t (&ent0)[kSlots / NT], RowOut &ro) {
+    constexpr int SL = kSlots / NT;
+    const int32_t tid = pv_tid<NT>();
+    const int32_t V = a.view;
+    const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
+    const uint64_t S_remove = pv_seed(2, t, uint32_t(r));
+    uint32_t keep = 0, removes = 0;
+    uint64_t hsum = 0;
+    bool kp[SL];
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+        const uint64_t e = ent0[i];
+        const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
+        const bool skip = e == kPvEmpty || x == uint32_t(r) || v == 0u;   // never list yourself
+        const bool rem = !skip && ((t5 - v) & 31u) >= tr;
+        kp[i] = !skip && !rem;
+        keep += kp[i] ? 1u : 0u;
+        removes += rem ? 1u : 0u;
+        if (rem) hsum += pv_hash(S_remove, x);
+    }
+    uint32_t total = 0;
+    uint32_t w = block_scan<NT>(keep, &total, sh.pre());
+    uint64_t *out = a.cur + int64_t(lr) * V;
+#pragma unroll
+    for (int i = 0; i < SL; ++i)
+        if (kp[i]) __builtin_nontemporal_store(ent0[i], out + w++);
+    for (int32_t i = int32_t(total) + tid; i < V; i += NT) __builtin_nontemporal_store(kPvEmpty, out + i);
+    ro.len = int32_t(total);
+    ro.removes = removes;
+    ro.hsum = hsum;
+    ro.written = true;
 }
 
 // workgroup-order index b -> row: b itself, or the b-th row of the k-descending order of
@@ -894,6 +935,17 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
         }
     }
     pm.mark(0);
+#ifndef GSP_PV_EXP_NO_OWN_ONLY
+    if constexpr (kExt == 0 && kQlo == 0) {
+        if (k == 0) {
+            pv_own_only<NT>(a, sh, r, lr, ent0, ro);
+            pm.mark(5);
+            pv_finish<NT>(a, sh, lr, k, k_all, false, ro);
+            pm.mark(6);
+            return;
+        }
+    }
+#endif
     // one variant per key count (own view + k sender views)
 #define GSP_PV_VARIANT(K)                                                                        \
     else if (kQlo <= K && K <= kQhi && k == K)                                                  \
