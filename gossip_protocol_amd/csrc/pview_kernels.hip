@@ -1132,6 +1132,9 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
 
 // Peers and sends of every row (one lane per row), after the tick kernel wrote the views:
 // min(F, len) distinct members by Philox rank-select over the id order, then the drop draw.
+// kF: the fan-out bound the peer arrays are sized for (4 covers config 5's f = 3 in a quarter of
+// the registers and compares of the general 16)
+template <int kF>
 __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
     if (lr >= a.rows) return;
@@ -1182,19 +1185,19 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
         return 0;
     };
     const int32_t keff = F < cnt ? F : cnt;
-    int32_t ch[16], dst[16];
+    int32_t ch[kF], dst[kF];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) { ch[q] = 0x7FFFFFFF; dst[q] = -1; }
+    for (int q = 0; q < kF; ++q) { ch[q] = 0x7FFFFFFF; dst[q] = -1; }
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
+    for (int kk = 0; kk < kF; ++kk) {
         if (kk >= keff) continue;
         const uint32_t u = draw_u31(kDomainPeer, a.seed, t, uint32_t(r), uint32_t(kk), 0u);
         int32_t rk = int32_t(u % uint32_t(cnt - kk));
 #pragma unroll
-        for (int q = 0; q < 16; ++q) rk += (q < kk && rk >= ch[q]) ? 1 : 0;   // ch ascending
+        for (int q = 0; q < kF; ++q) rk += (q < kk && rk >= ch[q]) ? 1 : 0;   // ch ascending
         int32_t x = rk;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {                   // insert rk, keeping ch ascending
+        for (int q = 0; q < kF; ++q) {                   // insert rk, keeping ch ascending
             const bool lt = x < ch[q];
             const int32_t c = ch[q];
             ch[q] = lt ? x : c;
@@ -1204,7 +1207,7 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     }
     uint32_t dropped = 0;
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
+    for (int kk = 0; kk < kF; ++kk) {
         if (kk >= F) continue;
         int32_t d = dst[kk];
         if (d >= 0) {
@@ -1285,7 +1288,14 @@ unsigned digest_blocks(int64_t records) {
 }
 
 void launch_send_and_digest(const PviewTickArgs &a, hipStream_t st) {
-    hipLaunchKernelGGL(pview_send_kernel, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
+#ifdef GSP_PV_EXP_SEND16
+    if (false)
+#else
+    if (a.fanout <= 4)
+#endif
+        hipLaunchKernelGGL(pview_send_kernel<4>, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL(pview_send_kernel<16>, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
     // the init tick's records hold only w3 (sends) -- its rowdig was zeroed by the host
     const int64_t records = int64_t(a.rows) * 4;
     hipLaunchKernelGGL(pview_digest_kernel, dim3(digest_blocks(records)), dim3(256), 0, st, a.rowdig,
