@@ -4,7 +4,13 @@
 //   K smallest senders in ascending order (the canonical receipt order; the rest is inbox
 //   overflow) as a fixed 8-slot record, so the tick kernel reaches the sender views after a
 //   single dependent load instead of three (offsets -> CSR -> rows).
-// pview_tick_kernel (one 256-lane workgroup per receiver row, ~21 KB of LDS):
+// pview_tick_split_kernel (the default form; rows bucketed by k, the number of messages a row
+//   merges, heavy rows first): k = 6, 7 as 256-lane rows in 20 KB of LDS, k = 5 / k = 4 as
+//   128-lane rows merged in place (one key buffer, 11.3 / 9.8 KB, PvSharedIP), k <= 3 as
+//   128-lane rows in 10 KB; k = 0 rows of the plain protocol skip steps 2-5 (pv_own_only).
+//   The grids are predicted on the host from an earlier tick's bucket sizes (no host wait);
+//   pview_tick_overflow_kernel runs the rows past a grid.  pview_tick_kernel is the one-kernel
+//   form (GSP_PV_SPLIT=0: one 256-lane workgroup per row, any k).  The row body:
 //   1. loads: the own view is requested first; the receipt record is read by every wave
 //      (no barrier) and the k sender views follow, one coalesced 2 KB row each;
 //   2. keys: each view is a sorted block of 256 slots of 32-bit keys id << 11 | source << 8
@@ -20,11 +26,14 @@
 //      ("orphan"); the lane whose id bracket holds it is the one that would hold its key,
 //      so found / not found is decided locally;
 //   5. survivors compacted in id order (one block scan); eviction to V by (age, -hb, id) with
-//      an age histogram, an hb histogram of the boundary age and an id-order tie prefix, all
-//      resolved by a single packed block scan over the lanes' survivors (kept in registers);
-//   6. the new sorted view is written back (2 KB, coalesced); Philox rank-select picks the
-//      peers; the row's digest counts go to a per-row record (no global atomics), summed by
-//      pview_digest_kernel.
+//      one histogram over (age, hb) bins, an exact hb histogram only for a boundary in an
+//      age's last bin, and an id-order tie prefix, resolved by a single packed block scan over
+//      the lanes' survivors (kept in registers);
+//   6. the new sorted view is written back (2 KB, coalesced); the row's digest counts go to a
+//      per-row record (no global atomics), summed by pview_digest_kernel.
+// pview_send_kernel (one lane per row): Philox rank-select peers over the new view, the drop
+//   draw, and each message's slot in its receiver's CSR segment (the deg atomic's return), so
+//   pview_scatter_kernel builds the next tick's receiver CSR without atomics.
 // HBM bytes per node-round: 2 * V * 8 (own view read + write) + k * V * 8 (sender views).
 #include <algorithm>
 #include <type_traits>
