@@ -62,13 +62,16 @@ def test_pview_eviction_bins_match_oracle(case):
 # each tick), 0 grids predicted from the last sizes seen + the overflow kernel (the default, no
 # host wait); GSP_TEST_PV_GRID_CAP caps the predicted grids, so the overflow kernel runs most
 # rows (3) or the tail of every bucket (50)
-@pytest.mark.parametrize("form", ["0:1:0", "1:1:0", "1:0:0", "1:0:3", "1:0:50"])
+# (round 3) a fourth field 0 turns off the one-shard receiver CSR scattered from the send
+# kernel's returned slots (GSP_PV_POS_SCATTER=0: the atomic fill-counter scatter instead)
+@pytest.mark.parametrize("form", ["0:1:0", "1:1:0", "1:0:0", "1:0:3", "1:0:50", "1:0:0:0"])
 @pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4]], ids=lambda c: "n%d_v%d" % c[:2])
 def test_pview_kernel_forms_match_oracle(case, form, monkeypatch):
-    split, sync, cap = form.split(":")
+    split, sync, cap, pos = (form.split(":") + ["1"])[:4]
     monkeypatch.setenv("GSP_PV_SPLIT", split)
     monkeypatch.setenv("GSP_PV_SPLITSYNC", sync)
     monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
+    monkeypatch.setenv("GSP_PV_POS_SCATTER", pos)
     _run_case(case)
 
 
