@@ -27,6 +27,7 @@ for i in 1 2; do
     for spec in ${AB:-base: exact:GSP_PV_SPLITSYNC=1}; do
         name=${spec%%:*}
         envs=${spec#*:}
+        envs=${envs//,/ }              # several settings: NAME=a,OTHER=b
         step ab_${name}_$i 150 env $envs python3 -u scripts/bench_pview.py --steps 20 --warmup 5 --no-cpu-baseline
         echo "$name $i $(tail -1 "$OUT/ab_${name}_$i.log" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("kernel_ms=%.3f csr_ms=%.3f step_ms=%.3f" % (d["roofline"]["kernel_ms_per_tick"], d["exchange_csr_ms"], d["ms_per_step"]))')"
     done
