@@ -23,7 +23,11 @@ enum : int { kPvRounds = 0, kPvMerges, kPvSent, kPvDropped, kPvDelivered, kPvOve
              kPvJoins, kPvRemoves, kPvEvicts, kPvHash, kPvFields };
 constexpr int kPvDigSlots = 256;   // spread the per-row digest atomics
 
-constexpr int kPvMaxSegment = 1024;  // messages one receiver can be sent in one tick
+// messages one receiver can be sent in one tick: the receipt kernel keeps the K smallest of any
+// number, so the bound is only the 16-bit per-row overflow field of the digest record (round 2
+// used 1024, which config 5's in-degree skew passes at tick ~73: the (age, -hb, id) eviction
+// order favours low ids, so a few nodes end up in most views)
+constexpr int kPvMaxSegment = 65535 + kPvMaxInbox;
 
 struct PviewTickArgs {
     const uint64_t *prev;        // view table of tick t-1 (this shard's rows)

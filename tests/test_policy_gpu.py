@@ -110,3 +110,37 @@ def test_partial_view_policies_match_oracle(case):
             assert np.array_equal(hb, hb_o) and np.array_equal(ts5, ts_o & 31), "row %d" % r
             if orc.fail_tick(r) >= ticks and orc.start_tick(r) <= ticks:
                 assert eng.own_hb(r) == orc.own_hb(r), "own hb row %d" % r
+
+
+def test_partial_view_join_burst_past_1024_messages():
+    """A join burst: 2,000 nodes start in one tick and all gossip to the introducer, so node 0
+    is sent ~1,800 messages in one tick -- past round 2's 1,024-message segment bound, which
+    made the job stop with a capacity error. The receipt kernel keeps the K smallest senders of
+    any number (include/gossip/gossip.h: the bound is now the digest's 16-bit overflow field):
+    every tick's digest, the message lists and the views equal oracle/pview_oracle.c, which has
+    no bound."""
+    n, ticks = 5000, 8
+    kw = dict(view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=RANDOM, fail_tick=6,
+              fail_ppm=20000, seed=43)
+    pol = dict(step_rate=0.0005, intro_list=8)
+    orc = PviewOracle(n, policy=oracle_policy(**pol), **kw)
+    burst = 0
+    with PviewEngine(n, max_ticks=ticks, policy=make_policy(**pol), **kw) as eng:
+        for t in range(1, ticks + 1):
+            src, dst = orc.messages()          # sent at t - 1, received at t
+            burst = max(burst, int(np.bincount(dst, minlength=n).max()))
+            want = orc.step()
+            eng.step(1)
+            got = eng.digest(t)
+            assert got == want, "tick %d\n got %s\nwant %s" % (t, got, want)
+            m = eng.messages()
+            src, dst = orc.messages()
+            assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+        for r in list(range(0, 40)) + list(range(40, n, 37)):
+            ids_o, hb_o, ts_o = orc.row(r)
+            buf, ln = eng.row(r)
+            ids, hb, ts5 = unpack_view(buf, ln)
+            assert ln == len(ids_o) and np.array_equal(ids, ids_o), "ids row %d" % r
+            assert np.array_equal(hb, hb_o) and np.array_equal(ts5, ts_o & 31), "row %d" % r
+    assert burst > 1024, "the case must send one receiver more than 1,024 messages (got %d)" % burst
