@@ -113,8 +113,9 @@ def test_partial_view_policies_match_oracle(case):
 
 
 def test_partial_view_join_burst_past_1024_messages():
-    """A join burst: 2,000 nodes start in one tick and all gossip to the introducer, so node 0
-    is sent ~1,800 messages in one tick -- past round 2's 1,024-message segment bound, which
+    """A join burst: 2,000 nodes start in one tick knowing only the introducer (no introducer
+    list, B = 0) and all gossip to it, so node 0 is sent up to ~2,450 messages per tick (oracle,
+    ticks 2-8) -- past round 2's 1,024-message segment bound, which
     made the job stop with a capacity error. The receipt kernel keeps the K smallest senders of
     any number (include/gossip/gossip.h: the bound is now the digest's 16-bit overflow field):
     every tick's digest, the message lists and the views equal oracle/pview_oracle.c, which has
@@ -122,7 +123,7 @@ def test_partial_view_join_burst_past_1024_messages():
     n, ticks = 5000, 8
     kw = dict(view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=RANDOM, fail_tick=6,
               fail_ppm=20000, seed=43)
-    pol = dict(step_rate=0.0005, intro_list=8)
+    pol = dict(step_rate=0.0005, intro_list=0)
     orc = PviewOracle(n, policy=oracle_policy(**pol), **kw)
     burst = 0
     with PviewEngine(n, max_ticks=ticks, policy=make_policy(**pol), **kw) as eng:
