@@ -38,7 +38,8 @@ struct PvShard {
     int32_t g = 0, row0 = 0, rows = 0;
     gsp::DevBuf<uint64_t> table[2];
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, out_pos, deg, off, fill, csr_src, err,
-        tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok;
+        tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok,
+        rows_run;                // tests (GSP_TEST_PV_COUNT_ROWS=1): rows run per tick
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     gsp::EvRing ev;
@@ -48,7 +49,7 @@ struct PvShard {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
         for (auto *b : {&own_hb, &fail_tick, &out_dst, &out_pos, &deg, &off, &fill, &csr_src, &err,
                         &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order, &start_tick, &ping,
-                        &joiners, &join_ok})
+                        &joiners, &join_ok, &rows_run})
             b->release();
         intro_buf.release();
         x.release();
@@ -157,6 +158,7 @@ struct gsp_pview {
         a.cus = cus;
         a.grid_margin = grid_margin;
         a.test_grid_cap = test_grid_cap;
+        a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.ev = sh.ev.args();
         return a;
     }
@@ -263,6 +265,10 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
+    if (const char *cr = std::getenv("GSP_TEST_PV_COUNT_ROWS"); cr && std::atoi(cr)) {
+        GSP_HIP(sh.rows_run.alloc(size_t(s->p.max_ticks + 1)));
+        GSP_HIP(hipMemsetAsync(sh.rows_run.p, 0, size_t(s->p.max_ticks + 1) * 4, st));
+    }
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
         GSP_HIP(sh.prof.alloc(64 * 8 * gsp::kPvProfPhases));
         GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * 8 * gsp::kPvProfPhases * 8, st));
@@ -411,8 +417,10 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         max_rows = std::max(max_rows, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
     s->pair_cap = max_rows;                       // a sender row goes to a shard at most once
     s->msg_cap = int64_t(max_rows) * p->fanout;
+    // the per-row overflow field of the digest record is 16 bits: k_all - k <= 65535
+    s->max_segment = std::min(gsp::kPvMaxSegment, 65535 + p->inbox);
     if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
-        s->max_segment = std::max(1, std::min(gsp::kPvMaxSegment, std::atoi(ms)));
+        s->max_segment = std::max(1, std::min(s->max_segment, std::atoi(ms)));
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
@@ -556,6 +564,11 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
                 GSP_HIP(hipMemcpyAsync(s->h_kseen + 8 * (&sh - s->local.data()), sh.kcount.p, 8 * 4,
                                        hipMemcpyDeviceToHost, s->st));
         }
+        // ranks: the receipt kernels' capacity flags, MAX over the ranks before any tick kernel
+        // of t reads them -- every rank's rows of t run, or none does, and every rank's flag
+        // (hence its sync) names the same tick
+        if (s->comm)
+            GSP_NCCL(ncclAllReduce(s->local[0].err.p, s->local[0].err.p, 1, ncclInt32, ncclMax, s->comm, s->st));
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));
         if (s->timing) {
@@ -651,6 +664,21 @@ int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n,
     for (PvShard &sh : s->local) GSP_HIP(sh.ev.drain(buf, cap, &total, &dropped));
     *n = total;
     if (lost) *lost = dropped;
+    return GSP_OK;
+}
+
+int gsp_pview_rows_run(gsp_pview *s, int32_t t, int64_t *rows) {
+    GSP_REQUIRE(s && rows && t >= 1 && t <= s->tick, GSP_ERR_INVALID, "gsp_pview_rows_run: tick %d", t);
+    GSP_REQUIRE(s->local[0].rows_run.p, GSP_ERR_INVALID,
+                "gsp_pview_rows_run: the engine counts no rows (set GSP_TEST_PV_COUNT_ROWS=1 before create)");
+    if (int rc = gsp_pview_sync(s)) return rc;
+    int64_t total = 0;
+    for (PvShard &sh : s->local) {
+        int32_t c = 0;
+        GSP_HIP(hipMemcpy(&c, sh.rows_run.p + t, 4, hipMemcpyDeviceToHost));
+        total += c;
+    }
+    *rows = total;
     return GSP_OK;
 }
 

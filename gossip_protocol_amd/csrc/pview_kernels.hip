@@ -904,6 +904,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
     constexpr int SL = kSlots / NT;
     const int32_t tid = pv_tid<NT>(), lane = tid & 63;
     const int32_t r = a.row0 + lr;
+    if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);     // tests: each row exactly once
     uint64_t ent0[SL];
 #pragma unroll
     for (int i = 0; i < SL; ++i)
@@ -1087,37 +1088,101 @@ __global__ void __launch_bounds__(kPvBlock, 8) pview_tick_overflow_kernel(PviewT
     }
 }
 
-// One lane per receiver row: the K smallest senders of its CSR segment, ascending.  With
-// a.kcount set, the rows are also bucketed by k (how many messages they merge): the tick
-// kernel then runs them k-descending, so each CU runs one code variant at a time.
+// The K smallest senders of every receiver's CSR segment, ascending (the canonical receipt
+// order; the rest is inbox overflow), as a fixed 8-slot record.  One lane per row, keeping a
+// sorted best 8: a sender not below the current 8th costs one compare (early reject), loads 4
+// at a time.  Rows past kPvWaveSegment senders (the hubs the eviction order makes: thousands of
+// senders at config 5 past tick ~70) are left to their wave, which runs them one after the
+// other: every lane keeps a best 8 of its stride of the segment, then 8 rounds of a wave
+// minimum pop the row's 8 smallest.  With a.kcount set, the rows are also bucketed by k (how
+// many messages they merge): the tick kernel then runs them k-descending.
+constexpr int32_t kPvWaveSegment = 64;
+
+// sender i of a segment and its row (>= 0 local, < 0 remote -slot - 1)
+__device__ __forceinline__ void pv_sender(const PviewReceiptArgs &a, int32_t o, int32_t &s, int32_t &sl) {
+    s = a.csr_src[o];
+    sl = a.csr_slot ? a.csr_slot[o] : s - a.row0;
+}
+
+// insertion into the ascending best 8 (bs, bl); a sender >= bs[7] changes nothing
+__device__ __forceinline__ void pv_best8(int32_t (&bs)[8], int32_t (&bl)[8], int32_t s, int32_t sl) {
+    if (s >= bs[7]) return;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const bool lt = s < bs[q];
+        const int32_t ts = bs[q], tl = bl[q];
+        bs[q] = lt ? s : ts;
+        bl[q] = lt ? sl : tl;
+        s = lt ? ts : s;
+        sl = lt ? tl : sl;
+    }
+}
+
+// the best 8 of senders [i0, k) with stride `step` of the segment at o0
+__device__ __forceinline__ void pv_best8_scan(const PviewReceiptArgs &a, int32_t o0, int32_t i0, int32_t k,
+                                              int32_t step, int32_t (&bs)[8], int32_t (&bl)[8]) {
+    int32_t i = i0;
+    for (; i + 3 * step < k; i += 4 * step) {        // four loads in flight
+        int32_t s[4], sl[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pv_sender(a, o0 + i + u * step, s[u], sl[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pv_best8(bs, bl, s[u], sl[u]);
+    }
+    for (; i < k; i += step) {
+        int32_t s, sl;
+        pv_sender(a, o0 + i, s, sl);
+        pv_best8(bs, bl, s, sl);
+    }
+}
+
+__device__ __forceinline__ int32_t wave_min_i32(int32_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x = min(x, __shfl_xor(x, d, 64));
+    return x;
+}
+
 __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) {
     const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
+    const int32_t lane = int32_t(threadIdx.x) & 63;
     const bool valid = lr < a.rows;
-    int32_t k = 0, k_all = 0;
+    int32_t k = 0, k_all = 0, o0 = 0;
+    int32_t bs[8], bl[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
+    bool wide = false;
     if (valid) {
-        const int32_t o0 = a.off[lr];
+        o0 = a.off[lr];
         k_all = a.off[lr + 1] - o0;
-        int32_t bs[8], bl[8];
+        if (k_all > a.max_segment) atomicCAS(a.err, 0, a.tick);   // this tick's tick kernel runs no row
+        else if (k_all > kPvWaveSegment) wide = true;
+        else pv_best8_scan(a, o0, 0, k_all, 1, bs, bl);
+        k = k_all > a.max_segment ? 0 : (k_all < a.inbox ? k_all : a.inbox);
+    }
+    // the wave's wide rows, one after the other (wave-uniform loop)
+    for (unsigned long long m = __ballot(wide); m; m &= m - 1) {
+        const int32_t l = __builtin_ffsll(m) - 1;
+        const int32_t wo = __builtin_amdgcn_readlane(o0, l), wk = __builtin_amdgcn_readlane(k_all, l);
+        int32_t ws[8], wl[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
-        if (k_all > a.max_segment) {
-            atomicCAS(a.err, 0, a.tick);        // this tick's tick kernel sees it and runs no row
-        } else {
-            for (int32_t i = 0; i < k_all; ++i) {             // insertion into the sorted best 8
-                int32_t s = a.csr_src[o0 + i];
-                int32_t sl = a.csr_slot ? a.csr_slot[o0 + i] : s - a.row0;
+        for (int q = 0; q < 8; ++q) { ws[q] = 0x7FFFFFFF; wl[q] = 0; }
+        pv_best8_scan(a, wo, lane, wk, 64, ws, wl);
+        // 8 rounds: the smallest head of the lanes' sorted lists (senders are distinct, so one
+        // lane holds it) goes to lane l's record, and that lane pops it
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const bool lt = s < bs[q];
-                    const int32_t ts = bs[q], tl = bl[q];
-                    bs[q] = lt ? s : ts;
-                    bl[q] = lt ? sl : tl;
-                    s = lt ? ts : s;
-                    sl = lt ? tl : sl;
-                }
+        for (int q = 0; q < 8; ++q) {
+            const int32_t mn = wave_min_i32(ws[0]);
+            const unsigned long long who = __ballot(ws[0] == mn && mn != 0x7FFFFFFF);
+            const int32_t src_slot = who ? __builtin_amdgcn_readlane(wl[0], __builtin_ffsll(who) - 1) : 0;
+            if (lane == l) { bs[q] = mn; bl[q] = src_slot; }
+            if (who && lane == __builtin_ffsll(who) - 1) {
+#pragma unroll
+                for (int z = 0; z < 7; ++z) { ws[z] = ws[z + 1]; wl[z] = wl[z + 1]; }
+                ws[7] = 0x7FFFFFFF;
             }
         }
-        k = k_all > a.max_segment ? 0 : (k_all < a.inbox ? k_all : a.inbox);
+    }
+    if (valid) {
         int4 *ps = reinterpret_cast<int4 *>(a.rc_src + int64_t(lr) * 8);
         int4 *pl = reinterpret_cast<int4 *>(a.rc_slot + int64_t(lr) * 8);
         ps[0] = make_int4(bs[0], bs[1], bs[2], bs[3]);

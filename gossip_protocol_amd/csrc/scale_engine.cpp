@@ -36,7 +36,9 @@ struct Shard {
     gsp::RowxBufs x;               // row layout exchange buffers
     gsp::DevBuf<uint16_t> table[2];
     gsp::DevBuf<int32_t> own_hb, fail_tick, cnt_total[2], cnt_slice, cnt_all, out_dst, picks,
-        ping, deg, off, fill, csr_src, err, tile_sum, start_tick, joiners, join_ok;
+        ping, deg, off, fill, csr_src, err, tile_sum, start_tick, joiners, join_ok,
+        long_list;                 // [2][1 + rows] by tick parity: rows with k > kMaxSegment
+                                   // (a CSR owner's: shard 0 of a shared group, else each)
     gsp::DevBuf<uint16_t> intro_buf;   // row layout, shards != 0: node 0's row of the last tick
     gsp::DevBuf<uint8_t> bitmap;
     gsp::DevBuf<unsigned long long> dig;
@@ -45,7 +47,7 @@ struct Shard {
     void release() {
         for (int b = 0; b < 2; ++b) { table[b].release(); cnt_total[b].release(); }
         for (auto *x : {&own_hb, &fail_tick, &cnt_slice, &cnt_all, &out_dst, &picks, &ping, &deg, &off,
-                        &fill, &csr_src, &err, &tile_sum, &start_tick, &joiners, &join_ok})
+                        &fill, &csr_src, &err, &tile_sum, &start_tick, &joiners, &join_ok, &long_list})
             x->release();
         intro_buf.release();
         bitmap.release();
@@ -73,7 +75,7 @@ struct gsp_scale {
     int32_t *h_cnt = nullptr, *h_recv = nullptr;   // pinned exchange counts (row layout)
     int32_t *h_err = nullptr;  // pinned mirror of the shards' capacity flags, refreshed by an
                                // async copy at the end of every gsp_scale_step call
-    int32_t max_segment = gsp::kMaxSegment;
+    int32_t max_segment = INT32_MAX;     // segments past kMaxSegment take the HBM sort
     ncclComm_t comm = nullptr; // one shard per process when set
     int64_t width = 0;         // n rounded up to 2048 * G
     int64_t stride = 0;        // columns per shard
@@ -83,6 +85,8 @@ struct gsp_scale {
     int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
     int32_t lds_pad = 0;       // GSP_SCALE_LDS_PAD: extra LDS per tick-kernel workgroup
     std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
+    gsp::DevBuf<gsp::ScaleTickArgs> long_tpl;   // [local][2]: every tile's args by tick parity
+                                                // (scale_long_kernel)
     std::vector<int32_t> h_fail, h_start;
     bool joins = false;        // a join schedule is set (some node starts after tick 0)
     gsp::JoinPlan plan;        // the joiners of every start tick
@@ -154,7 +158,16 @@ struct gsp_scale {
         a.err = local[0].err.p;        // one flag for every shard held here
         a.max_segment = max_segment;
         a.ev = sh.ev.args();
+        // the rows this tile's CSR defers (k > kMaxSegment): appended by the CSR's owner only
+        a.long_list = &sh == &owner(sh) ? long_list(sh, t) : nullptr;
         return a;
+    }
+
+    // the shard whose receiver CSR a shard reads (shared column tiles: shard 0's)
+    const Shard &owner(const Shard &sh) const { return shared ? local[0] : sh; }
+    int32_t *long_list(const Shard &sh, int32_t t) const {
+        const Shard &o = owner(sh);
+        return o.long_list.p + size_t(t & 1) * size_t(1 + o.rows);
     }
 
     gsp::ScaleResolveArgs resolve_args(Shard &sh, int32_t t) const {
@@ -243,6 +256,10 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     GSP_HIP(sh.csr_src.alloc(size_t(n) * s->p.fanout));
     GSP_HIP(sh.err.alloc(1));
     GSP_HIP(sh.tile_sum.alloc(size_t(n) / 4096 + 1));
+    if (!s->shared || &sh == &s->local[0]) {
+        GSP_HIP(sh.long_list.alloc(2 * (rows + 1)));
+        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 2 * (rows + 1) * 4, st));
+    }
     if (s->sliced && (!s->shared || &sh == &s->local[0])) {
         GSP_HIP(sh.cnt_slice.alloc(size_t(n)));
         GSP_HIP(sh.cnt_all.alloc(size_t(n) * s->shards * (s->shared ? 2 : 1)));
@@ -394,8 +411,10 @@ int exchange_rows(gsp_scale *s, int32_t t_sent) {
 // than max_segment messages sets the flag to the tick, and every later tick kernel returns at
 // once, so the job's state stays that of the tick before the overflow.  Every shard held by
 // this engine reads one flag (shard 0's); with a communicator the flag is exchanged each tick
-// (columns: inside the picks all-reduce; rows: with the exchange counts), so all ranks stop
-// together.
+// (columns: inside the picks all-reduce, and every rank holds the same receiver segments; rows:
+// all-reduced ahead of the tick kernels, and again with the exchange counts), so all ranks
+// stop at the same tick and report it from their own flag.  Without a test's bound
+// (GSP_TEST_MAX_SEGMENT) no segment overflows: segments past kMaxSegment are sorted in HBM.
 int mirrored_err(gsp_scale *s) {
     for (size_t i = 0; i < s->local.size(); ++i)
         GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
@@ -547,7 +566,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                     "327680 with events)", (long long)(s->stride / 8), p->events ? " + event stage" : "");
     }
     if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
-        s->max_segment = std::max(1, std::min(gsp::kMaxSegment, std::atoi(ms)));
+        s->max_segment = std::max(1, std::atoi(ms));
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
@@ -569,6 +588,20 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
         sh.row0 = s->rowmode ? gsp::rowx_row0(sh.g, p->n, shards) : 0;
         sh.rows = s->rowmode ? gsp::rowx_row0(sh.g + 1, p->n, shards) - sh.row0 : p->n;
         if (int rc = shard_alloc(s.get(), sh)) return rc;
+    }
+    {   // scale_long_kernel's tile table: each tile's args at both tick parities, digest base
+        // at tick 0, every tile reading its CSR owner's deferred-row list
+        std::vector<gsp::ScaleTickArgs> tpl;
+        for (Shard &sh : s->local)
+            for (int32_t par = 0; par < 2; ++par) {
+                gsp::ScaleTickArgs x = s->args(sh, 2 + par);
+                x.dig = sh.dig.p;
+                x.long_list = s->long_list(sh, par);
+                tpl.push_back(x);
+            }
+        GSP_HIP(s->long_tpl.alloc(tpl.size()));
+        GSP_HIP(hipMemcpy(s->long_tpl.p, tpl.data(), tpl.size() * sizeof(gsp::ScaleTickArgs),
+                          hipMemcpyHostToDevice));
     }
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_init(s->args(sh, 0), s->sliced, s->st));
     if (s->sliced)
@@ -638,6 +671,7 @@ int gsp_scale_destroy(gsp_scale *s) {
     }
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
     for (Shard &sh : s->local) sh.release();
+    s->long_tpl.release();
     if (s->comm) (void)ncclCommDestroy(s->comm);
     if (s->h_cnt) (void)hipHostFree(s->h_cnt);
     if (s->h_recv) (void)hipHostFree(s->h_recv);
@@ -670,6 +704,14 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
         }
         if (s->rowmode) {
             if (int rc = exchange_rows(s, t - 1)) return rc;
+            // ranks (row shards): a segment past a test's bound stops every rank's tick t, not
+            // only the holder's -- the flag is checked ahead of the tick kernel and all-reduced
+            // (ADVICE r03); unbounded otherwise (long segments are sorted in HBM)
+            if (s->comm && s->max_segment < INT32_MAX) {
+                Shard &sh = s->local[0];
+                GSP_HIP(gsp::launch_segment_check(sh.off.p, sh.rows, s->max_segment, sh.err.p, t, s->st));
+                GSP_NCCL(ncclAllReduce(sh.err.p, sh.err.p, 1, ncclInt32, ncclMax, s->comm, s->st));
+            }
         } else {
             for (Shard &sh : s->local) {
                 if (s->shared && &sh != &s->local[0]) continue;   // one CSR for every shard
@@ -684,6 +726,10 @@ int gsp_scale_step(gsp_scale *s, int32_t ticks) {
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
         for (Shard &sh : s->local)
             GSP_HIP(gsp::launch_scale_tick(s->args(sh, t), s->sliced, s->merge, s->st));
+        // the rows with more than kMaxSegment messages the launches above deferred (usually
+        // none: one short launch per tick)
+        GSP_HIP(gsp::launch_scale_long(s->args(s->local[0], t), s->long_tpl.p, int32_t(s->local.size()),
+                                       s->sliced, s->st));
         if (s->timing) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);

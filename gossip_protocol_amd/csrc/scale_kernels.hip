@@ -240,6 +240,41 @@ __device__ inline int32_t join_choose(const ScaleTickArgs &a, int32_t r, int32_t
     return found;
 }
 
+// A receiver segment longer than the LDS sort holds (k > kMaxSegment, e.g. a join burst on the
+// introducer): sorted in place in HBM by the row's workgroup into the canonical receipt order
+// (ascending sender; MP1Node::checkMessages drains a queue of any length, MP1Node.cpp:200-212),
+// slots moved along.  An all-ascending bitonic network over the next power of two: every
+// compare-exchange keeps the smaller key at the lower index, so the virtual +inf keys past k
+// never move and pairs reaching past k are skipped.  A segment belongs to one workgroup per
+// launch, and the launches that share a CSR (column tiles) run in stream order, so a later
+// launch re-sorts a sorted segment.
+__device__ inline void sort_long_segment(int32_t *src, int32_t *slot, int32_t k) {
+    int32_t P = 1;
+    while (P < k) P <<= 1;
+    for (int32_t size = 2; size <= P; size <<= 1) {
+        for (int32_t half = size >> 1; half > 0; half >>= 1) {
+            for (int32_t i = int32_t(threadIdx.x); i < (P >> 1); i += kScaleBlock) {
+                const int32_t b = i / half, o = i - b * half;
+                const bool flip = half == (size >> 1);   // pair i with its mirror in the block
+                const int32_t lo = flip ? b * size + o : b * 2 * half + o;
+                const int32_t hi = flip ? b * size + size - 1 - o : lo + half;
+                if (hi >= k) continue;
+                const int32_t x = src[lo], y = src[hi];
+                if (y < x) {
+                    src[lo] = y;
+                    src[hi] = x;
+                    if (slot) {
+                        const int32_t u = slot[lo];
+                        slot[lo] = slot[hi];
+                        slot[hi] = u;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // kPolicy bit 0: non-temporal own-row loads/stores; bit 1: non-temporal sender-row loads.
 // kPipe: software-pipelined chunk loads (the next chunk is requested before this one merges).
 // kTfail: TFAIL suspicion (a.tfail > 0): a sender's payload holds only the members it could
@@ -248,23 +283,29 @@ __device__ inline int32_t join_choose(const ScaleTickArgs &a, int32_t r, int32_t
 // kSwim: SWIM ping/ack probing (a.swim paths, oracle/scale_oracle.c): the probe this row sent at
 // t - 1 is resolved after the merges (answered: ts of the target = t; unanswered: ts = t -
 // TREMOVE, so the TREMOVE scan removes it), and wave 0 picks this tick's probe target.
-template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe = false, bool kTfail = false,
-          bool kSwim = false>
-__global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
+// The row's LDS (namespace scope: one set per kernel, shared by both row forms below).
+extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // fused: stride/32 words
+__shared__ int32_t s_src[kMaxSegment];
+__shared__ int32_t s_slot[kMaxSegment];
+__shared__ unsigned long long s_red[4][4];
+__shared__ int32_t s_jc[kMaxIntro];      // JOINREP payload: chosen columns / entries
+__shared__ uint32_t s_jv[kMaxIntro];
+__shared__ int32_t s_njc;
+__shared__ uint32_t s_evf[4];            // event stream: staged records per wave
+__shared__ unsigned long long s_evbase;
+
+// One row lr of the tick.  kLong: a row whose segment is longer than the LDS sort (k >
+// kMaxSegment, a join burst on the introducer), run by scale_long_kernel -- its own kernel,
+// because any share of its state in the tick kernel's body (one body with a runtime branch, an
+// inlined second copy, a called function) cost the plain rows registers: +1.1 % to +30 %
+// VGPRs or SGPR spills at config 3.  The tick kernel only defers such a row (a list entry).
+template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe, bool kTfail, bool kSwim,
+          bool kLong>
+__device__ __forceinline__ void scale_tick_row(const ScaleTickArgs &a, const int32_t lr) {
     constexpr bool kNtOwn = (kPolicy & 1) != 0, kNtSrc = (kPolicy & 2) != 0;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_bits[];   // fused: stride/32 words
-    __shared__ int32_t s_src[kMaxSegment];
-    __shared__ int32_t s_slot[kMaxSegment];
-    __shared__ unsigned long long s_red[4][4];
-    __shared__ int32_t s_jc[kMaxIntro];      // JOINREP payload: chosen columns / entries
-    __shared__ uint32_t s_jv[kMaxIntro];
-    __shared__ int32_t s_njc;
-    __shared__ uint32_t s_evf[4];            // event stream: staged records per wave
-    __shared__ unsigned long long s_evbase;
 
     const int32_t tid = threadIdx.x;
     const int32_t lane = tid & 63, wave = tid >> 6;
-    const int32_t lr = blockIdx.x;
     const int32_t r = a.row0 + lr;
     const int32_t t = a.tick;
     const int32_t F = a.fanout;
@@ -278,14 +319,32 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     }
 
     int32_t k = 0;
+    // a long segment (k > kMaxSegment): sorted in HBM, its first k - kMaxSegment messages are
+    // merged by the premerge below and the chunk loop merges the rest from LDS
+    constexpr bool lng = kLong;
     if (!kInit) {
         const int32_t o0 = a.off[lr];
         k = a.off[lr + 1] - o0;
-        if (k > a.max_segment) {
+        if (k > a.max_segment) {      // tests only (GSP_TEST_MAX_SEGMENT): a capacity error
             if (tid == 0) atomicCAS(a.err, 0, t);
             if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
             return;
         }
+#ifndef GSP_SCALE_EXP_NO_LONG          // A/B only: the tick kernel without the deferral
+        if (!lng && k > kMaxSegment) {   // deferred to scale_long_kernel (one list per CSR)
+            if (tid == 0 && a.long_list)
+                a.long_list[1 + atomicAdd(&a.long_list[0], 1)] = lr;
+            return;
+        }
+#endif
+    }
+    if constexpr (lng) {
+        const int32_t o0 = a.off[lr];
+        sort_long_segment(a.csr_src + o0, a.csr_slot ? a.csr_slot + o0 : nullptr, k);
+        if (tid == 0) s_src[0] = a.csr_src[o0];           // the JOINREP test below
+        __syncthreads();
+    } else if (!kInit) {
+        const int32_t o0 = a.off[lr];
         for (int32_t i = tid; i < k; i += kScaleBlock) s_src[i] = a.csr_src[o0 + i];
         __syncthreads();
         // canonical receipt order: ascending sender (senders are distinct per receiver)
@@ -311,7 +370,7 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     }
     // a JOINREP (sender kJoinRepSrc, sorted first) is merged apart from the GOSSIP loop: wave 0
     // resolves its payload columns, and the GOSSIPs are s_src[jr .. k)
-    const int32_t jr = (!kInit && k > 0 && s_src[0] == kJoinRepSrc) ? 1 : 0;
+    int32_t jr = (!kInit && k > 0 && s_src[0] == kJoinRepSrc) ? 1 : 0;
     if (jr) {
         if (wave == 0) {
             const int32_t nj = join_choose(a, r, t, s_jc, s_jv);
@@ -355,6 +414,80 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
     uint16_t *own_cur = a.cur + int64_t(lr) * stride;
     uint32_t live = 0, joins = 0, removes = 0;
     uint64_t hsum = 0;
+    if constexpr (lng) {
+        // Premerge of a long segment: the JOINREP and the GOSSIPs at sorted positions [jr, pend)
+        // merged in order into the own row, written to this tick's row (read back by the chunk
+        // loop as its own row, so the chunk loop merges senders [pend, k) after them: the same
+        // order).  The joins made here are counted here: absent before the tick, present after
+        // the premerge -- such an entry is fresh, and later merges only raise it, so the TREMOVE
+        // scan never removes it -- except the own column (cleared after the merges) and an
+        // unanswered probe target (made stale, then removed by the TREMOVE scan).
+        const int32_t o0 = a.off[lr], pend = k - kMaxSegment;
+        unsigned long long *const evb = (a.ev.buf && (a.ev.kinds & GSP_EVENTS_JOIN)) ? ev_stripe_buf(a.ev) : nullptr;
+        for (int64_t c0 = 0; c0 < stride; c0 += kChunk) {
+            const int64_t lc0 = c0 + int64_t(tid) * kEntriesPerLane, gc0 = a.col0 + lc0;
+            uint4 e = ld16<false>(own_prev + lc0);
+            const uint4 b = e;
+            if (jr) {
+                const int64_t d0 = -gc0;
+                if (d0 >= 0 && d0 < kEntriesPerLane)
+                    patch16(e, int(d0), [t5](uint32_t old) { return old ? ((((old >> 5) + 1u) << 5) | t5)
+                                                                        : ((1u << 5) | t5); });
+                for (int32_t q = 0; q < njc; ++q) {
+                    const int64_t dq = int64_t(s_jc[q]) - gc0;
+                    const uint32_t v = s_jv[q];
+                    if (dq >= 0 && dq < kEntriesPerLane)
+                        patch16(e, int(dq), [v, t5, tr](uint32_t old) { return merge_entry(old, v, t5, tr); });
+                }
+            }
+            for (int32_t j = jr; j < pend; ++j) {
+                const int32_t sj = a.csr_src[o0 + j];
+                const int32_t sl = a.csr_slot ? a.csr_slot[o0 + j] : sj - a.row0;
+                const uint16_t *row = sl >= 0 ? a.prev + int64_t(sl) * stride : a.remote + int64_t(-sl - 1) * stride;
+                uint4 v = ld16<false>(row + lc0);
+                if (kTfail) {
+                    v.x = gossiped(v.x);
+                    v.y = gossiped(v.y);
+                    v.z = gossiped(v.z);
+                    v.w = gossiped(v.w);
+                }
+                e.x = merge_word_scalar(e.x, v.x, t5, tr);
+                e.y = merge_word_scalar(e.y, v.y, t5, tr);
+                e.z = merge_word_scalar(e.z, v.z, t5, tr);
+                e.w = merge_word_scalar(e.w, v.w, t5, tr);
+                const int64_t ds = int64_t(sj) - gc0;
+                if (ds >= 0 && ds < kEntriesPerLane)
+                    patch16(e, int(ds), [t5](uint32_t old) { return (((old >> 5) + 1u) << 5) | t5; });
+            }
+            const uint32_t bw[4] = {b.x, b.y, b.z, b.w};
+            const uint32_t ew[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+            for (int i = 0; i < kEntriesPerLane; ++i) {
+                const int sh = (i & 1) * 16;
+                const int64_t col = gc0 + i;
+                const bool before = (bw[i >> 1] >> sh) & 0xFFFFu, after = (ew[i >> 1] >> sh) & 0xFFFFu;
+                if (!before && after && col != r && !(kSwim && col == pcol && pts != t5)) {
+                    joins++;
+                    hsum += event_mix(1, uint32_t(t), uint32_t(r), uint32_t(col));
+                    if (evb) {
+                        const unsigned long long p = atomicAdd(ev_stripe_count(a.ev), 1ull);
+                        if (int64_t(p) < a.ev.cap) evb[p] = event_record(1u, uint32_t(t), uint32_t(r), uint32_t(col));
+                    }
+                }
+            }
+            st16<false>(own_cur + lc0, ew);
+        }
+        // the chunk loop: the own row is the premerged one, the senders the last kMaxSegment
+        for (int32_t i = tid; i < kMaxSegment; i += kScaleBlock) {
+            const int32_t sj = a.csr_src[o0 + pend + i];
+            s_src[i] = sj;
+            s_slot[i] = a.csr_slot ? a.csr_slot[o0 + pend + i] : sj - a.row0;
+        }
+        __syncthreads();
+        own_prev = own_cur;
+        jr = 0;
+        k = kMaxSegment;
+    }
     // event stream: each wave stages its records as kind << 30 | column in LDS (after the
     // bitmap, kEvStage words per wave) and the row takes one ring reservation at its end; a
     // wave whose stage would overflow flushes it with a reservation of its own
@@ -594,10 +727,23 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
                     const int32_t c0 = a.cnt_prev[0];
                     merges += 1ull + uint64_t(a.intro_list < c0 ? a.intro_list : c0);
                 }
-                for (int32_t j = jr; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
+                // the whole segment (a long one's premerged part too, from the sorted CSR)
+                int32_t ka = k;
+                if constexpr (lng) {
+                    const int32_t o0 = a.off[lr];
+                    ka = a.off[lr + 1] - o0;
+                    if (a.csr_src[o0] == kJoinRepSrc) {   // the JOINREP went to the premerge
+                        const int32_t c0 = a.cnt_prev[0];
+                        merges += 1ull + uint64_t(a.intro_list < c0 ? a.intro_list : c0);
+                    }
+                    for (int32_t j = a.csr_src[o0] == kJoinRepSrc ? 1 : 0; j < ka; ++j)
+                        merges += 1ull + uint64_t(a.cnt_prev[a.csr_src[o0 + j]]);
+                } else {
+                    for (int32_t j = jr; j < k; ++j) merges += 1ull + uint64_t(a.cnt_prev[s_src[j]]);
+                }
                 atomicAdd(&dig[kDigRounds], 1ull);
                 atomicAdd(&dig[kDigMerges], merges);
-                atomicAdd(&dig[kDigDelivered], (unsigned long long)k);
+                atomicAdd(&dig[kDigDelivered], (unsigned long long)ka);
             }
             atomicAdd(&dig[kDigJoins], s_red[0][1] + s_red[1][1] + s_red[2][1] + s_red[3][1]);
             atomicAdd(&dig[kDigRemoves], s_red[0][2] + s_red[1][2] + s_red[2][2] + s_red[3][2]);
@@ -653,6 +799,37 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
             if (lane == 0) a.ping[lr] = p;
         }
     }
+}
+
+template <bool kInit, bool kSlice, int kMerge, int kPolicy, bool kPipe = false, bool kTfail = false,
+          bool kSwim = false>
+__global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a) {
+    scale_tick_row<kInit, kSlice, kMerge, kPolicy, kPipe, kTfail, kSwim, false>(a, int32_t(blockIdx.x));
+}
+
+// The rows the tick kernels deferred (k > kMaxSegment), after every tick-kernel launch of the
+// tick: tile g's args are its template of this tick's parity (made by the host at create) with
+// the tick's own fields; each tile's list is its CSR's (the tiles of an in-process group share
+// one).  Launched once per tick; without a deferred row every workgroup reads the counts and
+// exits.  It also clears the lists of the next tick's parity.
+template <bool kSlice, bool kTfail, bool kSwim>
+__global__ void __launch_bounds__(kScaleBlock) scale_long_kernel(ScaleTickArgs a, const ScaleTickArgs *tpl,
+                                                                 int32_t ntiles) {
+    const int32_t t = a.tick;
+    for (int32_t g = 0; g < ntiles; ++g) {
+        ScaleTickArgs ag = tpl[2 * g + (t & 1)];
+        ag.tick = t;
+        ag.drop_pct = a.drop_pct;
+        ag.drop_prev = a.drop_prev;
+        ag.dig += size_t(t) * kDigSlots * kDigFields;
+        const int32_t cnt = ag.long_list[0];
+        for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
+            scale_tick_row<false, kSlice, 1, 0, false, kTfail, kSwim, true>(ag, ag.long_list[1 + i]);
+            __syncthreads();                    // the row's LDS is read to its end
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int32_t g = 0; g < ntiles; ++g) tpl[2 * g + ((t + 1) & 1)].long_list[0] = 0;
 }
 
 // Column mode: one wave per sender.  The global member order of row s is the shards'
@@ -830,6 +1007,14 @@ __global__ void scatter_kernel(const int32_t *out_dst, int64_t slots, int32_t fa
     }
 }
 
+// the capacity test of the tick kernel, ahead of it (row shards of a communicator: the flag is
+// then all-reduced, so every rank's tick kernels of t see it)
+__global__ void segment_check_kernel(const int32_t *off, int32_t rows, int32_t max_segment, int32_t *err,
+                                     int32_t t) {
+    for (int32_t i = int32_t(blockIdx.x * blockDim.x + threadIdx.x); i < rows; i += int32_t(gridDim.x * blockDim.x))
+        if (off[i + 1] - off[i] > max_segment) atomicCAS(err, 0, t);
+}
+
 unsigned grid_for(int64_t items, int64_t per_block, int64_t cap) {
     int64_t b = (items + per_block - 1) / per_block;
     if (b > cap) b = cap;
@@ -896,6 +1081,28 @@ hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipS
     return hipGetLastError();
 }
 
+hipError_t launch_scale_long(const ScaleTickArgs &a, const ScaleTickArgs *tpl, int32_t ntiles, bool slice,
+                             hipStream_t st) {
+    if (ntiles < 1) return hipErrorInvalidValue;
+#ifdef GSP_SCALE_EXP_NO_LONG
+    return hipSuccess;
+#endif
+    const size_t lds = scale_lds_bytes(a.stride, slice, a.ev.buf != nullptr) + size_t(a.lds_pad);
+    const dim3 grid(64), block(kScaleBlock);
+    const int v = (slice ? 4 : 0) | (a.tfail > 0 ? 2 : 0) | (a.swim > 0 ? 1 : 0);
+    switch (v) {
+        case 0: hipLaunchKernelGGL((scale_long_kernel<false, false, false>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 1: hipLaunchKernelGGL((scale_long_kernel<false, false, true>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 2: hipLaunchKernelGGL((scale_long_kernel<false, true, false>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 3: hipLaunchKernelGGL((scale_long_kernel<false, true, true>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 4: hipLaunchKernelGGL((scale_long_kernel<true, false, false>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 5: hipLaunchKernelGGL((scale_long_kernel<true, false, true>), grid, block, lds, st, a, tpl, ntiles); break;
+        case 6: hipLaunchKernelGGL((scale_long_kernel<true, true, false>), grid, block, lds, st, a, tpl, ntiles); break;
+        default: hipLaunchKernelGGL((scale_long_kernel<true, true, true>), grid, block, lds, st, a, tpl, ntiles); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_scale_resolve(const ScaleResolveArgs &a, hipStream_t st) {
     if (a.stride % kChunk || a.shards < 1 || a.shards > 64 || a.fanout > 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(scale_resolve_kernel, dim3(unsigned((a.n + 3) / 4)), dim3(256), 0, st, a);
@@ -920,6 +1127,14 @@ hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, in
     hipLaunchKernelGGL(tile_sum_kernel, dim3(tiles), dim3(kScanThreads), 0, st, deg, n, tile_sum);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(tiles), dim3(kScanThreads), 0, st, deg, n, tile_sum,
                        off);
+    return hipGetLastError();
+}
+
+hipError_t launch_segment_check(const int32_t *off, int32_t rows, int32_t max_segment, int32_t *err,
+                                int32_t t, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(segment_check_kernel, dim3(grid_for(rows, 256, 1024)), dim3(256), 0, st, off, rows,
+                       max_segment, err, t);
     return hipGetLastError();
 }
 

@@ -24,7 +24,7 @@ constexpr int kScaleBlock = 256;          // 4 waves
 constexpr int kEntriesPerLane = 8;        // 16 B per lane per row chunk
 constexpr int kChunk = kScaleBlock * kEntriesPerLane;   // 2048 columns per block iteration
 constexpr int kEvStage = 512;             // event stream: LDS-staged records per wave (one chunk's worst case)
-constexpr int kMaxSegment = 1024;         // messages one receiver can merge per tick
+constexpr int kMaxSegment = 1024;         // receiver segments sorted in LDS; longer ones are sorted in HBM
 constexpr int kDigSlots = 64;             // atomic sharding of the per-tick digest
 enum : int { kDigRounds = 0, kDigMerges, kDigSent, kDigDropped, kDigDelivered, kDigJoins,
              kDigRemoves, kDigHash, kDigFields };
@@ -65,8 +65,9 @@ struct ScaleTickArgs {
     const int32_t *cnt_prev;     // [n] member counts at t-1 (global ids)
     int32_t *cnt_cur;            // [n] (fused: member count; slice: count in this slice)
     const int32_t *off;          // [rows + 1] receiver CSR
-    const int32_t *csr_src;      // sender ids
-    const int32_t *csr_slot;     // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
+    int32_t *csr_src;            // sender ids (a segment longer than kMaxSegment is sorted in
+                                 // place by its row's workgroup)
+    int32_t *csr_slot;           // row mode: >= 0 local row, < 0 remote row -slot-1 (or null)
     int32_t *out_dst;            // [rows * fanout]
     int32_t *deg;                // [n] messages per destination (atomic)
     int32_t *ping;               // swim: [rows] probe target of the last send (-1 none)
@@ -77,7 +78,11 @@ struct ScaleTickArgs {
     EvRingArgs ev;               // event stream (ev.buf null: off), event_ring.hpp
     int32_t *err;                // [1] capacity error: 0, else the first tick a receiver got
                                  // more than max_segment messages (every later tick is a no-op)
-    int32_t max_segment;         // <= kMaxSegment (lowered only by tests, GSP_TEST_MAX_SEGMENT)
+    int32_t max_segment;         // no bound (INT32_MAX) unless a test lowers it (GSP_TEST_MAX_SEGMENT)
+    int32_t *long_list;          // [1 + rows] of this tick's parity: count, then the rows whose
+                                 // segment is longer than kMaxSegment (deferred to
+                                 // scale_long_kernel); null: the tile appends nothing (the other
+                                 // tiles of a shared CSR)
 };
 
 __host__ __device__ inline unsigned long long event_record(uint32_t kind, uint32_t t, uint32_t r,
@@ -114,6 +119,10 @@ __device__ inline void wave_append_events(unsigned long long *buf, unsigned long
 // merge: 0 = per-entry scalar form, 1 = packed 16-bit form (v_pk_* / v_bfi_b32)
 hipError_t launch_scale_init(const ScaleTickArgs &a, bool slice, hipStream_t st);
 hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipStream_t st);
+// the rows every tick-kernel launch of this tick deferred (k > kMaxSegment): tpl[2 * g + parity]
+// = local tile g's args at tick parity (dig at tick 0); a = tile 0's args of this tick
+hipError_t launch_scale_long(const ScaleTickArgs &a, const ScaleTickArgs *tpl, int32_t ntiles, bool slice,
+                             hipStream_t st);
 
 // Column mode, after the all-gather of every shard's per-row slice counts:
 //   resolve: per sender, Philox rank-select over the global order of its members; the
@@ -149,6 +158,9 @@ hipError_t launch_max_into(int32_t *dst, const int32_t *src, int64_t count, hipS
 // off[0..n] = exclusive scan of deg[0..n); tile_sum holds ceil(n / 4096) ints of scratch
 hipError_t launch_exclusive_scan(const int32_t *deg, int32_t *off, int32_t n, int32_t *tile_sum,
                                  hipStream_t st);
+// err = t (if 0) when a receiver segment of off[rows + 1] is longer than max_segment
+hipError_t launch_segment_check(const int32_t *off, int32_t rows, int32_t max_segment, int32_t *err,
+                                int32_t t, hipStream_t st);
 // csr_src[off[d] + k] = sender, for every message slot i with out_dst[i] = d >= 0
 hipError_t launch_scatter(const int32_t *out_dst, int64_t slots, int32_t fanout, int32_t row0,
                           const int32_t *off, int32_t *fill, int32_t *csr_src, hipStream_t st);

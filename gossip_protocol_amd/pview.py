@@ -111,6 +111,12 @@ class PviewEngine:
         """(records, lost) since the last drain (events=True); see _lib.split_events."""
         return _lib.drain_events(lib().gsp_pview_drain_events, self._h)
 
+    def rows_run(self, t):
+        """Tests: rows the tick kernels of tick t ran (GSP_TEST_PV_COUNT_ROWS=1 at create)."""
+        v = ctypes.c_int64()
+        check(lib().gsp_pview_rows_run(self._h, t, ctypes.byref(v)), "gsp_pview_rows_run")
+        return v.value
+
     def perf(self):
         p = _lib.GspScalePerf()
         check(lib().gsp_pview_perf_get(self._h, ctypes.byref(p)), "gsp_pview_perf_get")

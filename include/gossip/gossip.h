@@ -197,8 +197,9 @@ int gsp_exact_stats_get(gsp_engine *e, gsp_exact_stats *out);
 /* ------------------------------------------------------------------------------------
  * Driver policies of the scale engines.  The reference hard-codes them in
  * its driver -- node i starts at tick (int)(STEP_RATE * i) (Application.cpp:143,
- * Params.cpp:30), messages are dropped in the window t in [50, 300) (Application.cpp:177,
- * 198), one random node or N/2 contiguous nodes crash at t = 100 (Application.cpp:180-196);
+ * Params.cpp:30), messages are dropped from the end of t = 50 to the end of t = 300, i.e.
+ * the sends of ticks [51, 301) (Application.cpp:177, 198: fail() sets and clears the flag
+ * after that tick's mp1Run), one random node or N/2 contiguous nodes crash at t = 100 (Application.cpp:180-196);
  * the scale engines take them as data, run on the device.  All zeros = the pre-joined,
  * always-dropping, single-event protocol of ABI 2.
  * ---------------------------------------------------------------------------------- */
@@ -456,6 +457,10 @@ int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);
 /* As gsp_scale_drain_events (join / remove / evict records). */
 int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
+/* Test diagnostics: the rows the tick kernels of tick t ran, summed over the shards held here
+ * -- every row exactly once in every launch form, so it equals the rows held.  Needs the
+ * environment variable GSP_TEST_PV_COUNT_ROWS=1 at create (else GSP_ERR_INVALID). */
+int gsp_pview_rows_run(gsp_pview *s, int32_t t, int64_t *rows);
 
 #ifdef __cplusplus
 }

@@ -145,3 +145,54 @@ def test_partial_view_join_burst_past_1024_messages():
             assert ln == len(ids_o) and np.array_equal(ids, ids_o), "ids row %d" % r
             assert np.array_equal(hb, hb_o) and np.array_equal(ts5, ts_o & 31), "row %d" % r
     assert burst > 1024, "the case must send one receiver more than 1,024 messages (got %d)" % burst
+
+
+@pytest.mark.parametrize("layout,shards,tfail,swim,events", [
+    ("columns", 1, 0, 0, False), ("columns", 3, 0, 0, True), ("rows", 2, 0, 0, True),
+    ("columns", 1, 5, 2, True)], ids=["fused", "columns3_events", "rows2_events", "tfail_swim_events"])
+def test_full_view_join_burst_past_1024_messages(layout, shards, tfail, swim, events):
+    """The full view's join burst: 2,000 nodes start in one tick knowing
+    only the introducer (B = 0) and all gossip to it, so node 0 is sent ~2,000 messages a tick --
+    past the tick kernel's LDS sort of 1,024 senders, which round 3 turned into a capacity
+    error.  The reference drains a queue of any length (MP1Node.cpp:200-212); the kernel now
+    sorts such a segment in HBM and merges its first k - 1,024 messages in a premerge pass
+    (scale_kernels.hip).  Every tick's digest, the message lists, every row of the hub and of
+    sampled nodes, and (events on) every tick's join / remove records equal
+    oracle/scale_oracle.c, which has no bound -- in the fused, column-group and row layouts,
+    with TFAIL and SWIM."""
+    from gossip_protocol_amd import _lib
+    n, ticks = 5000, 8
+    kw = dict(fanout=3, drop_pct=10, fail_mode=RANDOM, fail_tick=6, fail_ppm=20000, seed=43,
+              tfail=tfail, swim=swim)
+    pol = dict(step_rate=0.0005, intro_list=0)
+    orc = ScaleOracle(n, policy=oracle_policy(**pol), **kw)
+    burst = 0
+    with ScaleEngine(n, max_ticks=ticks, group=shards, layout=layout, policy=make_policy(**pol),
+                     events=events, **kw) as eng:
+        if events:
+            eng.drain_events()
+        for t in range(1, ticks + 1):
+            src, dst = orc.messages()          # sent at t - 1, received at t
+            burst = max(burst, int(np.bincount(dst, minlength=n).max()))
+            want = orc.step()
+            eng.step(1)
+            got = eng.digest(t)
+            assert got == want, "tick %d\n got %s\nwant %s" % (t, got, want)
+            if events:
+                rec, lost = eng.drain_events()
+                assert lost == 0
+                k, tk, r, x = _lib.split_events(rec)
+                ok, orr, ox = orc.events()
+                assert sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                    sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), "events tick %d" % t
+            m = eng.messages()
+            src, dst = orc.messages()
+            assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+        for r in list(range(0, 8)) + list(range(8, n, 41)):
+            pres_o, hb_o, ts_o = orc.row(r)
+            pres_d, hb_d, ts5_d = unpack(eng.row(r))
+            assert np.array_equal(pres_d, pres_o.astype(bool)), "presence row %d" % r
+            assert np.array_equal(hb_d[pres_d], hb_o[pres_d]), "hb row %d" % r
+            assert np.array_equal(ts5_d[pres_d], ts_o[pres_d] & 31), "ts row %d" % r
+    assert burst > 1024, "the case must send one receiver more than 1,024 messages (got %d)" % burst

@@ -75,6 +75,64 @@ def test_pview_kernel_forms_match_oracle(case, form, monkeypatch):
     _run_case(case)
 
 
+# the no-wait forms with the event stream on (the overflow kernel runs the
+# rows past a grid; a row run twice would duplicate its event records, which digests and views
+# cannot see) and a per-tick count of the rows the tick kernels ran, which must be every row
+# exactly once (GSP_TEST_PV_COUNT_ROWS=1, gsp_pview_rows_run)
+@pytest.mark.parametrize("form", ["1:0:3", "1:0:50", "1:0:0", "1:1:0", "0:1:0"])
+@pytest.mark.parametrize("case", [CASES[1], CASES[3]], ids=lambda c: "n%d_v%d" % c[:2])
+def test_pview_kernel_forms_events_and_rows_run(case, form, monkeypatch):
+    from gossip_protocol_amd import _lib
+    split, sync, cap = form.split(":")
+    monkeypatch.setenv("GSP_PV_SPLIT", split)
+    monkeypatch.setenv("GSP_PV_SPLITSYNC", sync)
+    monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
+    kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+              fail_ppm=ppm, seed=seed, tremove=10)
+    orc = PviewOracle(n, **kw)
+    kinds = set()
+    with PviewEngine(n, max_ticks=ticks, events=True, **kw) as eng:
+        eng.drain_events()
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d" % t
+            assert eng.rows_run(t) == n, "tick %d: the tick kernels ran %d rows of %d" % (
+                t, eng.rows_run(t), n)
+            rec, lost = eng.drain_events()
+            assert lost == 0
+            k, tk, r, x = _lib.split_events(rec)
+            assert np.all(tk == t)
+            ok, orr, ox = orc.events()
+            assert sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), "events tick %d" % t
+            kinds |= set(ok.tolist())
+    assert kinds == {1, 2, 3}                           # joins, removes and evictions
+
+
+def test_pview_rows_run_queued_ticks(monkeypatch):
+    """gsp_pview_step(k) queues k ticks without a host wait, every later tick predicted from
+    older bucket sizes: still every row exactly once per tick, with and without the test cap."""
+    for cap in ("0", "50"):
+        monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
+        monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+        n = 20000
+        with PviewEngine(n, view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=5,
+                         fail_ppm=50000, seed=3, max_ticks=16) as eng:
+            eng.step(16)
+            assert [eng.rows_run(t) for t in range(1, 17)] == [n] * 16
+
+
+def test_pview_rows_run_needs_the_env():
+    from gossip_protocol_amd._lib import GspError
+    with PviewEngine(500, view=32, max_ticks=2) as eng:
+        eng.step(1)
+        with pytest.raises(GspError, match="GSP_TEST_PV_COUNT_ROWS"):
+            eng.rows_run(1)
+
+
 def _run_case(case, h0=1):
     n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
     kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,

@@ -405,8 +405,9 @@ def test_scale_full_size_properties():
 
 
 def test_capacity_error_stops_the_job(monkeypatch):
-    """A receiver sent more messages than the kernel's segment bound (1,024; lowered to 2 here
-    through the test-only GSP_TEST_MAX_SEGMENT) stops the job loudly: the device flags the
+    """A receiver sent more messages than a test's segment bound (none by default -- round 4:
+    segments past the LDS sort's 1,024 are sorted in HBM; lowered to 2 here through the
+    test-only GSP_TEST_MAX_SEGMENT) stops the job loudly: the device flags the
     tick and every later tick kernel runs no row.  The flag reaches the host by an async copy
     at the end of each step call: sync() and every read return GSP_ERR_CAPACITY, and so does
     every gsp_scale_step call made after the copy landed -- never state computed from a
@@ -442,8 +443,8 @@ def test_rccl_rank_path_tiled(tiles, variant):
     if variant == "tfail_swim":
         kw.update(tfail=5, swim=2)
     if variant == "policy_events":
-        # 20 joiners a tick (step_rate 0.05): every new node gossips to the introducer first, so
-        # a burst of > 1024 joiners in one tick would overflow node 0's segment (capacity error)
+        # 20 joiners a tick (step_rate 0.05): every new node gossips to the introducer first
+        # (a burst of > 1024 joiners: test_policy_gpu.py::test_full_view_join_burst_*)
         pol = dict(drop_window=(2, 9), step_rate=0.05, intro_list=4, fail_events=[(8, 3, 0)])
     orc = ScaleOracle(n, policy=oracle_policy(**pol) if pol else None, **kw)
     with ScaleEngine(n, max_ticks=ticks, rank=0, world=1, nccl_id=nccl_unique_id(), tiles=tiles,
