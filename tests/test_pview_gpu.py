@@ -322,3 +322,43 @@ def test_pview_full_size_properties():
             assert np.array_equal(gi, ids), "ids of row %d (%d senders)" % (r, len(senders[r]))
             assert np.array_equal(gh, hb), "hb of row %d" % r
             assert np.array_equal(gt, ts), "ts of row %d" % r
+
+
+def test_pview_eight_row_shards_full_size():
+    """BASELINE config 5 at full size as 8 row shards in one process: the
+    multi-GPU layout's pack / gather / CSR / exchange kernels with the RCCL send / recv
+    replaced by device copies -- the best proxy of the 8-GPU run on a one-GPU box.  Every
+    tick's digest equals the one-shard engine's, sampled views are identical, and the bytes
+    that cross shards per tick (the per-(sender, shard) deduplicated sender views plus the
+    12-byte message records, EmulNet.cpp:87-177 across shards) are reported next to DESIGN's
+    estimate of 4.2 GB per tick at G = 8."""
+    import json
+    import os
+    n, ticks, G = 1 << 20, 12, 8
+    kw = dict(view=256, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=10,
+              fail_ppm=50000, seed=0x5EED)
+    rng = np.random.default_rng(8)
+    sample = sorted(set(rng.integers(0, n, 300).tolist()) | {0, 1, n - 1, n // G, n // G - 1})
+    with PviewEngine(n, max_ticks=ticks, **kw) as one:
+        one.step(ticks)
+        want = [one.digest(t) for t in range(1, ticks + 1)]
+        rows = {r: one.row(r) for r in sample}
+    with PviewEngine(n, max_ticks=ticks, group=G, **kw) as eng:
+        assert eng.layout() == (G, 0, 0, n)
+        xgmi = []
+        for t in range(1, ticks + 1):
+            before = eng.perf()["xgmi_bytes"]
+            eng.step(1)
+            xgmi.append(eng.perf()["xgmi_bytes"] - before)
+            assert eng.digest(t) == want[t - 1], "tick %d" % t
+        for r in sample:
+            buf, ln = eng.row(r)
+            assert ln == rows[r][1] and np.array_equal(buf, rows[r][0]), "row %d" % r
+    # every tick after the first moves each alive sender's view to ~2 other shards
+    assert all(x > 1e9 for x in xgmi[1:]), xgmi
+    rec = {"n": n, "shards": G, "ticks": ticks, "xgmi_bytes_per_tick": xgmi}
+    out = os.environ.get("GSP_TEST_RECORD_DIR")
+    if out:
+        with open(os.path.join(out, "pview_rows8_xgmi.json"), "w") as f:
+            json.dump(rec, f)
+    print(json.dumps(rec))
