@@ -100,7 +100,8 @@ class GspPviewParams(ctypes.Structure):
                 ("drop_pct", c_int32), ("tremove", c_int32), ("h0", c_int32),
                 ("fail_mode", c_int32), ("fail_tick", c_int32), ("fail_ppm", c_int32),
                 ("seed", c_uint64), ("max_ticks", c_int32), ("tfail", c_int32), ("swim", c_int32),
-                ("policy", GspPolicy), ("events", c_int32), ("event_cap", c_int64)]
+                ("policy", GspPolicy), ("events", c_int32), ("event_cap", c_int64),
+                ("evict_order", c_int32)]
 
 
 class GspPviewDigest(ctypes.Structure):

@@ -17,8 +17,8 @@
 //   SCALE_N n | FANOUT f | VIEW V | INBOX K | TREMOVE t | TFAIL t | SWIM s | H0 h | SEED u64 |
 //   TICKS t | STEP_RATE x | INTRO_LIST B | DROP_PCT p | DROP_WINDOW from until |
 //   FAIL tick mode ppm (repeatable; mode RANDOM|BLOCK|SINGLE|HALF|0-4; the first FAIL line
-//   replaces the SINGLE_FAILURE event) | EVENTS 0|1 | EVENT_CAP n
-// Full view: VIEW / INBOX are refused.  Partial view: every key applies.
+//   replaces the SINGLE_FAILURE event) | EVENTS 0|1 | EVENT_CAP n | EVICT_ORDER 0|1
+// Full view: VIEW / INBOX / EVICT_ORDER are refused.  Partial view: every key applies.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,7 +31,7 @@ namespace {
 
 struct ConfAll {
     int32_t n = 0, fanout = 3, view = 256, inbox = 7, tremove = 20, tfail = 0, swim = 0, h0 = 1;
-    int32_t drop_pct = 0, ticks = 700, events = 0;
+    int32_t drop_pct = 0, ticks = 700, events = 0, evict_order = 0;
     int64_t event_cap = 0;
     uint64_t seed = 0x5EED;
     gsp_fail_event first{100, GSP_FAIL_SINGLE, 0};
@@ -98,6 +98,7 @@ int read_conf(const char *path, ConfAll &c) {
         else if (k == "FANOUT") one(&c.fanout);
         else if (k == "VIEW") { one(&c.view); c.have_view = true; }
         else if (k == "INBOX") { one(&c.inbox); c.have_view = true; }
+        else if (k == "EVICT_ORDER") { one(&c.evict_order); c.have_view = true; }
         else if (k == "TREMOVE") one(&c.tremove);
         else if (k == "TFAIL") one(&c.tfail);
         else if (k == "SWIM") one(&c.swim);
@@ -143,7 +144,7 @@ int gsp_scale_params_from_conf(const char *path, gsp_scale_params *out) {
     GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_scale_params_from_conf: out is NULL");
     ConfAll c;
     if (int rc = read_conf(path, c)) return rc;
-    GSP_REQUIRE(!c.have_view, GSP_ERR_INVALID, "%s: VIEW / INBOX are partial-view keys", path);
+    GSP_REQUIRE(!c.have_view, GSP_ERR_INVALID, "%s: VIEW / INBOX / EVICT_ORDER are partial-view keys", path);
     std::memset(out, 0, sizeof *out);
     out->n = c.n;
     out->fanout = c.fanout;
@@ -185,6 +186,7 @@ int gsp_pview_params_from_conf(const char *path, gsp_pview_params *out) {
     out->policy = c.pol;
     out->events = c.events;
     out->event_cap = c.event_cap;
+    out->evict_order = c.evict_order;
     return GSP_OK;
 }
 

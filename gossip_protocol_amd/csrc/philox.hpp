@@ -17,6 +17,7 @@ enum : uint32_t {
     kDomainPeer = 0x50454552u,  // "PEER": scale-mode peer choice
     kDomainPing = 0x50494E47u,  // "PING": SWIM probe target and probe paths
     kDomainJoin = 0x4A4F494Eu,  // "JOIN": the members a JOINREP carries (bounded introducer list)
+    kDomainEvict = 0x45564354u, // "EVCT": the eviction tie rotation of a row (evict_order 1)
 };
 
 // Sequential sampling without replacement: draw k maps u % (cnt - k) onto the ranks not

@@ -159,6 +159,7 @@ struct gsp_pview {
         a.grid_margin = grid_margin;
         a.test_grid_cap = test_grid_cap;
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
+        a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
         return a;
     }
@@ -212,6 +213,8 @@ int pview_validate(const gsp_pview_params *p) {
     GSP_REQUIRE(p->swim >= 0 && p->swim <= 8, GSP_ERR_INVALID, "swim=%d: 0 (off) or 1..8 paths", p->swim);
     GSP_REQUIRE(p->events >= 0 && p->events <= 15, GSP_ERR_INVALID, "events=%d: 0 off, 1 all, or an OR of GSP_EVENTS_*", p->events);
     GSP_REQUIRE(p->event_cap >= 0, GSP_ERR_INVALID, "event_cap=%lld", (long long)p->event_cap);
+    GSP_REQUIRE(p->evict_order == 0 || p->evict_order == 1, GSP_ERR_INVALID,
+                "evict_order=%d: 0 (age, -hb, id) or 1 (rotated id ties)", p->evict_order);
     return gsp::validate_policy(p->policy, p->n);
 }
 

@@ -67,9 +67,11 @@ constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: abov
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
 static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
 
-// Event digest term (oracle/pview_oracle.c gsp_pv_event_mix): a row seed per kind (1 join,
-// 2 remove, 3 evict), computed once per row, and a three-multiply finaliser of the member id
-// per event (a row hashes ~1000 events per tick).
+// Event digest term (oracle/pview_oracle.c gsp_pv_event_mix): S + g(x) per event, S a row seed
+// per kind (1 join, 2 remove, 3 evict) and g(x) = ((x ^ lo32(S)) * 0x9E3779B1) >> 5.  A row
+// hashes ~1000 events per tick, so the per-event part is one multiply (round 4; it was a
+// three-multiply 64-bit finaliser): lanes sum g(x) in 32 bits (< 2^27 each, at most 30 per
+// lane) and pv_finish adds the S terms once per wave, as the wave's event counts times S.
 __device__ inline uint64_t pv_seed(uint32_t kind, uint32_t t, uint32_t r) {
     uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) | (uint64_t(r & 0x1FFFFF) << 21);
     z += 0x9E3779B97F4A7C15ull;
@@ -77,17 +79,19 @@ __device__ inline uint64_t pv_seed(uint32_t kind, uint32_t t, uint32_t r) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ inline uint64_t pv_hash(uint64_t S, uint32_t x) {
+__device__ inline uint32_t pv_hash(uint32_t s, uint32_t x) {
 #ifdef GSP_PV_EXP_NOHASH
     return 0;
 #endif
-    uint32_t a = (x ^ uint32_t(S)) * 0x9E3779B1u;
-    a ^= a >> 16;
-    a *= 0x85EBCA6Bu;
-    a ^= a >> 13;
-    uint32_t b = a * 0xC2B2AE35u;
-    b ^= b >> 16;
-    return S + ((uint64_t(b) << 32) | a);
+#ifdef GSP_PV_EXP_OLDHASH    // A/B only (round 3's per-event finaliser; not the oracle's digest)
+    uint32_t h = (x ^ s) * 0x9E3779B1u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    uint32_t b = h * 0xC2B2AE35u;
+    return (b ^ (b >> 16) ^ h) >> 5;
+#endif
+    return ((x ^ s) * 0x9E3779B1u) >> 5;
 }
 
 // the reference's merge of one payload entry (packed hb << 5 | ts5, 0 = absent)
@@ -289,7 +293,7 @@ struct RowOut {
     int32_t ids_off, vals_off;
     int32_t len;
     uint32_t joins, removes, evicts, merged;
-    uint64_t hsum;
+    uint32_t hsum;                // sum of g(x) over the lane's events (pv_hash)
     bool written;                 // the view is already in HBM (pv_own_only)
 };
 
@@ -323,6 +327,7 @@ __device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r,
 // SWIM (pcol / pok: the probe of t - 1, target id or kNoId, answered) and the event stream;
 // the plain protocol (config 5) runs the kernel without them.
 constexpr int kExtEv = 1, kExtPol = 2;   // kExt bits: event stream; TFAIL / SWIM / JOINREP
+constexpr int kExtRot = 4;               // eviction ties by the rotated id (evict_order 1)
 template <int kBlocks, int kExt, int NT, class Sh>
 __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int32_t r,
                                              int32_t k, const uint64_t (&ent0)[kSlots / NT],
@@ -339,8 +344,8 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
     const uint32_t th0 = t + uint32_t(a.h0);
     const int32_t Pe = (k + 1) * kSlots;                // keys that can be real
-    const uint64_t S_join = pv_seed(1, t, uint32_t(r)), S_remove = pv_seed(2, t, uint32_t(r)),
-                   S_evict = pv_seed(3, t, uint32_t(r));
+    const uint32_t S_join = uint32_t(pv_seed(1, t, uint32_t(r))), S_remove = uint32_t(pv_seed(2, t, uint32_t(r))),
+                   S_evict = uint32_t(pv_seed(3, t, uint32_t(r)));
 
     // ---- 2. keys: one sorted block of 256 slots per source ------------------------------------
     // block 0 = the own view (loaded with the record), block m = message m's payload: the
@@ -505,10 +510,17 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     const uint32_t lo_id = tid > 0 ? key_id(prev_key) + 1u : 0u;   // this lane brackets ids
     const uint32_t hi_id = tid < NT - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
 
-    uint32_t res[Q], rid[Q];
+    // res / rid[e]: the lane's surviving entry of key e (0: none).  128-lane rows (kMO): slot Q
+    // takes the shift when the lane's one adopted orphan is inserted in id order (below), so the
+    // survivor passes visit Q + 1 slots instead of Q slots plus an orphan test before each; the
+    // 256-lane rows keep the orphan apart (their one more slot spills at 64 VGPRs)
+    constexpr bool kMO = NT == 128;
+    constexpr int QS = kMO ? Q + 1 : Q;
+    uint32_t res[QS], rid[QS];
+    if constexpr (kMO) res[Q] = rid[Q] = 0;
     uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
     uint32_t jmask = 0, rmask = 0;                       // event stream: join / remove keys
-    uint64_t hsum = 0;
+    uint32_t hsum = 0;
     // the run being folded: id, value, own-view value, sender event (message index, applied)
     uint32_t ax = kNoId, av = 0, ae0 = 0, ajs = 0;
     bool aown = false, adone = false;
@@ -620,13 +632,25 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             if ((adopt >> jj) & 1u) { o_x = ssrc[jj]; o_p = ains[jj]; }
     }
     const bool multi = __ballot(n_orph > 1) != 0ull;          // wave-uniform
-    // rb[e]: the eviction bin of res[e] (filled on the eviction path, computed once per slot)
-    uint32_t rb[Q];
+    if (kMO && !multi) {  // the lane's orphan (if any) into res / rid at its id position o_p
 #pragma unroll
-    for (int e = 0; e < Q; ++e) rb[e] = 0;
+        for (int e = QS - 1; e >= 0; --e) {
+            const bool shift = o_p >= 0 && e > o_p;
+            res[e] = e == o_p ? fresh : shift ? res[e > 0 ? e - 1 : 0] : res[e];
+            rid[e] = e == o_p ? o_x : shift ? rid[e > 0 ? e - 1 : 0] : rid[e];
+        }
+    }
+    // rb[e]: the eviction bin of res[e] (filled on the eviction path, computed once per slot)
+    uint32_t rb[QS];
+#pragma unroll
+    for (int e = 0; e < QS; ++e) rb[e] = 0;
     const uint32_t fresh_bin = pv_bin(fresh, t5, th0);
     auto for_each = [&](auto &&f) {                            // f(value, id, bin)
-        if (!multi) {
+        if (kMO && !multi) {
+#pragma unroll
+            for (int e = 0; e < QS; ++e)
+                if (res[e]) f(res[e], rid[e], rb[e]);
+        } else if (!multi) {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
                 if (o_p == e) f(fresh, o_x, fresh_bin);
@@ -659,7 +683,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         ro.len = int32_t(total);
     } else {
 #pragma unroll
-        for (int e = 0; e < Q; ++e) rb[e] = pv_bin(res[e], t5, th0);
+        for (int e = 0; e < QS; ++e) rb[e] = pv_bin(res[e], t5, th0);
         for_each([&](uint32_t, uint32_t, uint32_t b) {
             atomicAdd(&bins[b >> 1], 1u << ((b & 1u) * 16u));
         });
@@ -736,35 +760,71 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         }
         pm.mark(8);
         // one packed scan: ties before this lane (low 16) and plain keeps before it (high 16)
-        uint32_t nt = 0, nk = 0;
+        uint32_t nt = 0, nk = 0, nth = 0;
+        // evict_order 1 (kExtRot): the ties are kept in the order of the rotated id (x - m) mod
+        // n -- the ties with x >= m in id order, then those below m -- so nth counts the ties
+        // at or above m; m = Philox(EVICT; t, r) mod n (oracle/pview_oracle.c pv_rot)
+        const uint32_t mrot = (kExt & kExtRot) ? draw_u31(kDomainEvict, a.seed, t, uint32_t(r), 0u, 0u) %
+                                                     uint32_t(a.n)
+                                               : 0u;
         // ties: the boundary bin's entries with hb == hstar (all of them unless e >= 31);
         // plain keeps: lower bins, and boundary-bin entries with a larger hb or without a tie
-        for_each([&](uint32_t v, uint32_t, uint32_t b) {
+        auto count = [&](uint32_t v, uint32_t x, uint32_t b, bool ok) {
             const uint32_t hb = v >> 5;
-            const bool is_tie = tie && b == bstar && hb == hstar;
+            const bool is_tie = ok && tie && b == bstar && hb == hstar;
             nt += is_tie ? 1u : 0u;
-            nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
-        });
+            if (kExt & kExtRot) nth += (is_tie && x >= mrot) ? 1u : 0u;
+            nk += (ok && !is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
+        };
+        if (kMO && !multi) {                                 // predicated, no branches
+#pragma unroll
+            for (int e = 0; e < QS; ++e) count(res[e], rid[e], rb[e], res[e] != 0u);
+        } else {
+            for_each([&](uint32_t v, uint32_t x, uint32_t b) { count(v, x, b, true); });
+        }
         pm.mark(9);
         uint32_t sums = 0;
         const uint32_t ex = block_scan<NT>(nt | (nk << 16), &sums, scan_buf + 4);
         pm.mark(10);
         uint32_t tie_before = ex & 0xFFFFu;
-        const uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
+        uint32_t ties_kept_before = tie_before < need2 ? tie_before : need2;
+        // rotated order: keep_hi of the ties at or above m, keep_lo below it; before this lane
+        // in id order come lo_before ties below m, then hi_before at or above it
+        uint32_t hi_before = 0, keep_hi = 0, keep_lo = 0;
+        if ((kExt & kExtRot) && tie) {                       // block-uniform
+            uint32_t A = 0;
+            hi_before = block_scan<NT>(nth, &A, scan_buf);   // scan_buf's last reads retired
+            keep_hi = need2 < A ? need2 : A;
+            keep_lo = need2 - keep_hi;
+            const uint32_t lo_before = tie_before - hi_before;
+            ties_kept_before = (lo_before < keep_lo ? lo_before : keep_lo) + (hi_before < keep_hi ? hi_before : keep_hi);
+        }
         uint32_t w = (ex >> 16) + (tie ? ties_kept_before : 0u);
         uint32_t *Wid = sh.wids(cur);
         uint16_t *Wval = sh.wvals(cur);
         uint64_t evp = 0;                                  // event stream: this lane's evictions
         const bool ev_on = (kExt & kExtEv) && a.ev.buf && (a.ev.kinds & GSP_EVENTS_EVICT);
         if (ev_on) {
-            const int32_t tk = int32_t(need2) - int32_t(tie_before);
-            const uint32_t kept = nk + uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
-            evp = wave_reserve_events(ev_stripe_count(a.ev), nloc - kept);
+            uint32_t kept_t;
+            if ((kExt & kExtRot) && tie) {
+                const uint32_t lo_before = tie_before - hi_before, ntl = nt - nth;
+                const int32_t kl = int32_t(keep_lo) - int32_t(lo_before), kh = int32_t(keep_hi) - int32_t(hi_before);
+                kept_t = uint32_t(kl <= 0 ? 0 : (kl >= int32_t(ntl) ? int32_t(ntl) : kl)) +
+                         uint32_t(kh <= 0 ? 0 : (kh >= int32_t(nth) ? int32_t(nth) : kh));
+            } else {
+                const int32_t tk = int32_t(need2) - int32_t(tie_before);
+                kept_t = uint32_t(tk <= 0 ? 0 : (tk >= int32_t(nt) ? int32_t(nt) : tk));
+            }
+            evp = wave_reserve_events(ev_stripe_count(a.ev), nloc - (nk + kept_t));
         }
+        uint32_t lo_rank = tie_before - hi_before;           // kExtRot: ranks among the ties
         for_each([&](uint32_t v, uint32_t x, uint32_t b) {
             const uint32_t hb = v >> 5;
             bool keep = b < bstar || (b == bstar && (!tie || hb > hstar));
-            if (tie && b == bstar && hb == hstar) keep = tie_before++ < need2;
+            if (tie && b == bstar && hb == hstar) {
+                if (kExt & kExtRot) keep = x >= mrot ? hi_before++ < keep_hi : lo_rank++ < keep_lo;
+                else keep = tie_before++ < need2;
+            }
             if (keep) {
                 Wid[w] = x;
                 Wval[w] = uint16_t(v);
@@ -819,7 +879,10 @@ __device__ __forceinline__ void pv_finish(const PviewTickArgs &a, Sh &sh, int32_
     const uint64_t jr = jrs;                          // joins | removes << 16
     const uint64_t ev = evm & 0xFFFFu;
     uint64_t mg = evm >> 16;
-    const uint64_t h = wave_sum64(ro.hsum);
+    // the wave's event hash: its g(x) sum plus its event counts times the row's kind seeds
+    const uint32_t r = uint32_t(a.row0 + lr);
+    const uint64_t h = wave_sum64(ro.hsum) + uint64_t(jrs & 0xFFFFu) * pv_seed(1, t, r) +
+                       uint64_t(jrs >> 16) * pv_seed(2, t, r) + uint64_t(ev) * pv_seed(3, t, r);
     if (lane == 0) {
         uint64_t w0 = mg, w1 = jr | (ev << 32);
         if (wave == 0) {
@@ -853,9 +916,9 @@ __device__ __forceinline__ void pv_own_only(const PviewTickArgs &a, Sh &sh, int3
     const int32_t tid = pv_tid<NT>();
     const int32_t V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
-    const uint64_t S_remove = pv_seed(2, t, uint32_t(r));
+    const uint32_t S_remove = uint32_t(pv_seed(2, t, uint32_t(r)));
     uint32_t keep = 0, removes = 0;
-    uint64_t hsum = 0;
+    uint32_t hsum = 0;
     bool kp[SL];
 #pragma unroll
     for (int i = 0; i < SL; ++i) {
@@ -946,7 +1009,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
     }
     pm.mark(0);
 #ifndef GSP_PV_EXP_NO_OWN_ONLY
-    if constexpr (kExt == 0 && kQlo == 0) {
+    if constexpr ((kExt & ~kExtRot) == 0 && kQlo == 0) {   // (a row without messages evicts nothing)
         if (k == 0) {
             pv_own_only<NT>(a, sh, r, lr, ent0, ro);
             pm.mark(5);
@@ -1409,7 +1472,7 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
     // the protocol extensions in use select the kernel: kExtPol for TFAIL / SWIM / joins,
     // kExtEv for the event stream (the plain protocol runs neither)
     const int ext = ((a.tfail > 0 || a.swim > 0 || a.start_tick != nullptr) ? kExtPol : 0) |
-                    (a.ev.buf != nullptr ? kExtEv : 0);
+                    (a.ev.buf != nullptr ? kExtEv : 0) | (a.evict_rot ? kExtRot : 0);
     if (a.order && a.split) {
         // split form: k = 6, 7 / k = 5 / k = 4 / k <= 3 (pview_tick_split_kernel), in this order
         // (the heavy rows first).  Grids: the exact bucket sizes, read back synchronously
@@ -1479,11 +1542,13 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         if (ext != 0) return hipErrorNotSupported;
         GSP_PV_SPLIT_LAUNCH(0);
 #else
-        switch (ext) {
+        switch (ext) {      // evict_order 1: the plain protocol's kernel, or the superset one
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
             case kExtEv: GSP_PV_SPLIT_LAUNCH(kExtEv); break;
             case kExtPol: GSP_PV_SPLIT_LAUNCH(kExtPol); break;
-            default: GSP_PV_SPLIT_LAUNCH(kExtPol | kExtEv); break;
+            case kExtPol | kExtEv: GSP_PV_SPLIT_LAUNCH(kExtPol | kExtEv); break;
+            case kExtRot: GSP_PV_SPLIT_LAUNCH(kExtRot); break;
+            default: GSP_PV_SPLIT_LAUNCH(kExtRot | kExtPol | kExtEv); break;
         }
 #endif
 #undef GSP_PV_SPLIT_LAUNCH
@@ -1502,7 +1567,8 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         case 0: hipLaunchKernelGGL((pview_tick_kernel<0>), g, blk, 0, st, a); break;
         case kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtEv>), g, blk, 0, st, a); break;
         case kExtPol: hipLaunchKernelGGL((pview_tick_kernel<kExtPol>), g, blk, 0, st, a); break;
-        default: hipLaunchKernelGGL((pview_tick_kernel<kExtPol | kExtEv>), g, blk, 0, st, a); break;
+        case kExtPol | kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtPol | kExtEv>), g, blk, 0, st, a); break;
+        default: hipLaunchKernelGGL((pview_tick_kernel<kExtRot | kExtPol | kExtEv>), g, blk, 0, st, a); break;
     }
 #endif
     launch_send_and_digest(a, st);

@@ -74,6 +74,7 @@ struct PviewTickArgs {
                                  // + 1024 (GSP_PV_GRID_MARGIN, percent)
     int32_t test_grid_cap;       // tests only (GSP_TEST_PV_GRID_CAP): cap on every predicted
                                  // split grid, so the overflow kernel runs most rows (0: none)
+    int32_t evict_rot;           // evict_order 1: eviction ties by the rotated id (gossip.h)
     int32_t *rows_run;           // tests only (GSP_TEST_PV_COUNT_ROWS=1): [1] counter of this
                                  // tick, +1 per row a tick kernel runs (every row exactly once,
                                  // in every launch form), or null

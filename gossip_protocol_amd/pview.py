@@ -36,14 +36,15 @@ class PviewEngine:
     def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
                  fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, max_ticks=256, device=0,
                  group=1, rank=0, world=1, nccl_id=None, tfail=0, swim=0, policy=None,
-                 events=False, event_cap=0, params=None):
+                 events=False, event_cap=0, evict_order=0, params=None):
         if params is None:
             params = _lib.GspPviewParams(n=n, view=view, fanout=fanout, inbox=inbox,
                                          drop_pct=drop_pct, tremove=tremove, h0=h0,
                                          fail_mode=fail_mode, fail_tick=fail_tick,
                                          fail_ppm=fail_ppm, seed=seed, max_ticks=max_ticks,
                                          tfail=tfail, swim=swim, policy=policy or _lib.GspPolicy(),
-                                         events=int(events), event_cap=event_cap)
+                                         events=int(events), event_cap=event_cap,
+                                         evict_order=evict_order)
         self.params = params
         n, view, fanout = params.n, params.view, params.fanout
         self._h = ctypes.c_void_p()

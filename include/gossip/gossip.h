@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 3
+#define GSP_ABI_VERSION 4
 
 typedef enum {
     GSP_OK = 0,
@@ -420,6 +420,11 @@ typedef struct {
     gsp_policy policy;    /* as gsp_scale_params                                         */
     int32_t events;       /* as gsp_scale_params, with GSP_EVENTS_EVICT (gsp_pview_drain_events) */
     int64_t event_cap;    /* as gsp_scale_params                                          */
+    int32_t evict_order;  /* 0: a view past `view` keeps the smallest (age, -hb, id) -- the
+                             default, and the order every headline number is quoted on; 1:
+                             ties of (age, hb) broken by the rotated id (id - m) mod n, m =
+                             Philox(EVICT; t, r) mod n, so no id is favoured (the id order makes
+                             low ids hubs) */
 } gsp_pview_params;
 
 typedef struct {

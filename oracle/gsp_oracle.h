@@ -147,6 +147,8 @@ typedef struct {
     uint64_t seed;
     int32_t tfail, swim;   /* as gsp_scale_cfg */
     gsp_oracle_policy pol;
+    int32_t evict_order;   /* 0: ties by id; 1: by the rotated id (x - m) mod n, m =
+                              Philox(EVICT; t, r) mod n (gsp_pview_params.evict_order) */
 } gsp_pview_cfg;
 
 typedef struct {

@@ -22,6 +22,7 @@
 #define GSP_DOMAIN_PEER 0x50454552u /* "PEER": scale-mode peer choice     */
 #define GSP_DOMAIN_PING 0x50494E47u /* "PING": SWIM probe target / paths  */
 #define GSP_DOMAIN_JOIN 0x4A4F494Eu /* "JOIN": bounded introducer list     */
+#define GSP_DOMAIN_EVICT 0x45564354u /* "EVCT": eviction tie rotation (evict_order 1) */
 
 static inline void gsp_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2],
                                      uint32_t out[4]) {

@@ -55,18 +55,13 @@ static int gossipable(const gsp_pview_cfg *c, int32_t t, int32_t ts) {
     return c->tfail <= 0 || t - ts < c->tfail;
 }
 
-/* Event digest term of the partial view (kinds: 1 join, 2 remove, 3 evict).  A row seed
- * S = gsp_event_mix(kind, t, r, 0) and a three-multiply 32-bit finaliser of the member id:
- * the kernel hashes ~1000 events per row per tick, so the per-event part stays cheap. */
+/* Event digest term of the partial view (kinds: 1 join, 2 remove, 3 evict): S + g(x), a row
+ * seed S = gsp_event_mix(kind, t, r, 0) and g(x) = ((x ^ lo32(S)) * 0x9E3779B1) >> 5 -- the
+ * kernel hashes ~1000 events per row per tick, so the per-event part is one multiply (round 4;
+ * the sum over a row's events is still a 64-bit checksum: the S terms are 64-bit). */
 uint64_t gsp_pv_event_mix(int kind, int64_t t, int64_t r, int64_t x) {
     const uint64_t S = gsp_event_mix(kind, t, r, 0);
-    uint32_t a = ((uint32_t)x ^ (uint32_t)S) * 0x9E3779B1u;
-    a ^= a >> 16;
-    a *= 0x85EBCA6Bu;
-    a ^= a >> 13;
-    uint32_t b = a * 0xC2B2AE35u;
-    b ^= b >> 16;
-    return S + (((uint64_t)b << 32) | a);
+    return S + ((((uint32_t)x ^ (uint32_t)S) * 0x9E3779B1u) >> 5);
 }
 
 static const pv_ent *find_id(const pv_ent *l, int32_t len, int32_t id) {
@@ -229,12 +224,18 @@ static int cmp_i32(const void *a, const void *b) {
     return (x > y) - (x < y);
 }
 
-typedef struct { pv_ent e; int32_t age; } keyed;
+/* eviction order (age, -hb, tie key): the tie key is the id, or with evict_order 1 the id
+ * rotated by the row's Philox draw (pv_rot) -- no id favoured by every row */
+typedef struct { pv_ent e; int32_t age; int32_t tk; } keyed;
 static int cmp_keep(const void *a, const void *b) {
     const keyed *x = a, *y = b;
     if (x->age != y->age) return x->age < y->age ? -1 : 1;
     if (x->e.hb != y->e.hb) return x->e.hb > y->e.hb ? -1 : 1;
-    return (x->e.id > y->e.id) - (x->e.id < y->e.id);
+    return (x->tk > y->tk) - (x->tk < y->tk);
+}
+static int32_t pv_rot(const gsp_pview_cfg *c, int32_t t, int32_t r) {
+    return (int32_t)(gsp_philox_u31(GSP_DOMAIN_EVICT, c->seed, (uint32_t)t, (uint32_t)r, 0, 0) %
+                     (uint32_t)c->n);
 }
 static int cmp_id(const void *a, const void *b) {
     const pv_ent *x = a, *y = b;
@@ -306,7 +307,12 @@ static int32_t pv_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r, const p
         res[nres++] = cur;
     }
     if (nres > V) {
-        for (int32_t i = 0; i < nres; ++i) { kk[i].e = res[i]; kk[i].age = t - res[i].ts; }
+        const int32_t m = c->evict_order ? pv_rot(c, t, r) : 0;
+        for (int32_t i = 0; i < nres; ++i) {
+            kk[i].e = res[i];
+            kk[i].age = t - res[i].ts;
+            kk[i].tk = c->evict_order ? (res[i].id - m + c->n) % c->n : res[i].id;
+        }
         qsort(kk, nres, sizeof(keyed), cmp_keep);
         for (int32_t i = V; i < nres; ++i) {
             d->evicts++;

@@ -68,7 +68,7 @@ class PviewCfg(ctypes.Structure):
                 ("tremove", ctypes.c_int32), ("h0", ctypes.c_int32), ("fail_mode", ctypes.c_int32),
                 ("fail_tick", ctypes.c_int32), ("fail_ppm", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("tfail", ctypes.c_int32), ("swim", ctypes.c_int32),
-                ("pol", Policy)]
+                ("pol", Policy), ("evict_order", ctypes.c_int32)]
 
 
 class PviewDigest(ctypes.Structure):
@@ -340,10 +340,11 @@ class PviewOracle:
         return k[:n], r[:n], x[:n]
 
     def __init__(self, n, view=256, fanout=3, inbox=7, drop_pct=0, tremove=20, h0=1,
-                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, tfail=0, swim=0, policy=None):
+                 fail_mode=0, fail_tick=10, fail_ppm=0, seed=0x5EED, tfail=0, swim=0, policy=None,
+                 evict_order=0):
         self.L = load_oracle()
         self.cfg = PviewCfg(n, view, fanout, inbox, drop_pct, tremove, h0, fail_mode, fail_tick,
-                            fail_ppm, seed, tfail, swim, policy or Policy())
+                            fail_ppm, seed, tfail, swim, policy or Policy(), evict_order)
         self.h = self.L.gsp_pview_oracle_create(ctypes.byref(self.cfg))
         assert self.h, "pview oracle create failed"
         self.n, self.view = n, view

@@ -11,6 +11,11 @@ cases (the sharded form of EmulNet::ENsend / ENrecv, /root/reference/EmulNet.cpp
                   ranks by grouped ncclSend / ncclRecv, counts by all-gather / broadcast,
                   node 0's row by ncclBroadcast (join schedule)
   pview_rows      partial view, row shards: the same exchange for sender views
+  pview_capacity, rows_capacity
+                  a test's segment bound (GSP_TEST_MAX_SEGMENT) that a receiver of one rank
+                  passes first: every rank's sync() must raise GSP_ERR_CAPACITY at the same
+                  step, naming the same tick (the flag is all-reduced before the
+                  tick kernels read it)
 
 Every rank runs the engine and the CPU oracle on the same inputs.  torch.distributed (gloo)
 carries only the RCCL id and the digests.  Checks: each tick's digest summed over ranks
@@ -54,6 +59,8 @@ def run(case):
     uid = broadcast_bytes(nccl_unique_id() if rank == 0 else None)
     ticks = 12
     bad = []
+    if case in ("pview_capacity", "rows_capacity"):
+        return run_capacity(case, rank, world, dev, uid)
     if case in ("columns_tiled", "rows"):
         n = 8192
         kw = dict(fanout=3, drop_pct=10, fail_mode=RANDOM, fail_tick=4, fail_ppm=20000, seed=8,
@@ -130,6 +137,39 @@ def run(case):
         print(json.dumps({"case": case, "world": world, "ranks": res}), flush=True)
     dist.destroy_process_group()
     return 0 if not any(r["bad"] for r in res) else 1
+
+
+def run_capacity(case, rank, world, dev, uid):
+    import torch.distributed as dist
+    from gossip_protocol_amd._lib import GspError
+    from gossip_protocol_amd.scale import ScaleEngine
+    os.environ["GSP_TEST_MAX_SEGMENT"] = "9"     # in-degree ~ Poisson(3): a few receivers pass 9
+    if case == "pview_capacity":
+        from gossip_protocol_amd.pview import PviewEngine
+        eng = PviewEngine(20000, view=64, fanout=3, inbox=5, seed=13, max_ticks=30, device=dev,
+                          rank=rank, world=world, nccl_id=uid)
+    else:
+        eng = ScaleEngine(8192, fanout=3, seed=8, max_ticks=30, device=dev, rank=rank, world=world,
+                          nccl_id=uid, layout="rows")
+    stop = None
+    for t in range(1, 31):
+        eng.step(1)
+        try:
+            eng.sync()
+        except GspError as e:
+            import re
+            m = re.search(r"at tick (\d+)", str(e))
+            stop = (t, int(m.group(1)) if m else str(e)[:200])
+            break
+    eng.close()
+    res = [None] * world
+    dist.all_gather_object(res, {"rank": rank, "stop": stop})
+    ok = stop is not None and all(r["stop"] == res[0]["stop"] for r in res)
+    if rank == 0:
+        print(json.dumps({"case": case, "world": world, "ranks": [dict(r, bad=[] if ok else ["stop"])
+                                                                   for r in res]}), flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

@@ -123,7 +123,7 @@ def test_struct_layouts_match_the_header():
                       ("gsp_pview_params", _lib.GspPviewParams),
                       ("gsp_pview_digest", _lib.GspPviewDigest)]:
         assert L.gsp_struct_size(name.encode()) == ctypes.sizeof(cls), name
-    assert L.gsp_abi_version() == 3
+    assert L.gsp_abi_version() == 4
 
 
 def test_scale_params_from_reference_conf():
@@ -158,9 +158,10 @@ def test_scale_params_extended_keys(tmp_path):
     assert (p.policy.drop_from, p.policy.drop_until, p.policy.intro_list) == (3, 30, 8)
     assert abs(p.policy.step_rate - 0.01) < 1e-12 and (p.tfail, p.swim, p.events) == (5, 2, 1)
     with open(path, "a") as f:
-        f.write("VIEW: 64\nINBOX: 5\n")
+        f.write("VIEW: 64\nINBOX: 5\nEVICT_ORDER: 1\n")
     q = pv_conf(path)
     assert (q.n, q.view, q.inbox, q.fanout, q.tfail, q.swim) == (4096, 64, 5, 5, 5, 2)
+    assert q.evict_order == 1
     L = _lib.lib()
     assert L.gsp_scale_params_from_conf(path.encode(), ctypes.byref(_lib.GspScaleParams())) == -1
     assert b"partial-view" in L.gsp_last_error()

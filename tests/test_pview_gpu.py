@@ -133,10 +133,36 @@ def test_pview_rows_run_needs_the_env():
             eng.rows_run(1)
 
 
-def _run_case(case, h0=1):
+# evict_order 1 (round 4): eviction ties by the rotated id (x - m) mod n, m = Philox(EVICT; t, r)
+# mod n -- the plain protocol's kernel with the kExtRot bit, and the superset kernel with events
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[3]], ids=lambda c: "n%d_v%d" % c[:2])
+def test_pview_rotated_eviction_matches_oracle(case):
+    _run_case(case, evict_order=1)
+
+
+def test_pview_rotated_eviction_events_match_oracle():
+    from gossip_protocol_amd import _lib
+    n, ticks = 2000, 30
+    kw = dict(view=48, fanout=3, inbox=5, drop_pct=20, fail_mode=1, fail_tick=6, fail_ppm=30000,
+              seed=23, tremove=12, evict_order=1)
+    orc = PviewOracle(n, **kw)
+    with PviewEngine(n, max_ticks=ticks, events=True, **kw) as eng:
+        eng.drain_events()
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d" % t
+            rec, lost = eng.drain_events()
+            k, tk, r, x = _lib.split_events(rec)
+            ok, orr, ox = orc.events()
+            assert sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), "events tick %d" % t
+
+
+def _run_case(case, h0=1, evict_order=0):
     n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
     kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
-              fail_ppm=ppm, seed=seed, h0=h0)
+              fail_ppm=ppm, seed=seed, h0=h0, evict_order=evict_order)
     orc = PviewOracle(n, **kw)
     rng = np.random.default_rng(seed)
     with PviewEngine(n, max_ticks=ticks, **kw) as eng:

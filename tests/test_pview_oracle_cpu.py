@@ -35,3 +35,31 @@ def test_row_step_equals_oracle_step():
             overflowed += dr["overflow"] > 0
         assert d["node_rounds"] > 0
     assert checked > 500 and overflowed > 0
+
+
+def test_rotated_eviction_keeps_the_rotated_id_prefix():
+    """evict_order 1: among entries tied on (age, hb) the kept ones are those first in the
+    rotated id order (x - m) mod n, m = Philox(EVICT; t, r) mod n -- here a row whose own view
+    (V entries) and one sender's view (V more, all fresh, same hb) tie everywhere, so exactly
+    the V smallest rotated ids survive; with evict_order 0 the V smallest ids."""
+    from tests.oracle_binding import Policy, load_oracle
+    n, V, t, r, seed = 5000, 32, 7, 1234, 99
+    rng = np.random.default_rng(3)
+    ids = np.sort(rng.choice(np.arange(n)[np.arange(n) != r], 2 * V, replace=False))
+    own_ids, snd_ids = np.sort(ids[::2]), np.sort(ids[1::2])
+    sender = int(snd_ids[0])
+    snd_view_ids = np.sort(np.concatenate([snd_ids[1:], [own_ids[0]]]))   # the sender skips itself
+    hb = lambda a: np.full(len(a), 5, np.int32)
+    ts = lambda a: np.full(len(a), t - 1, np.int32)
+    for order in (0, 1):
+        cfg = PviewCfg(n, V, 3, 7, 0, 20, 1, 0, 10, 0, seed, 0, 0, Policy(), order)
+        (gi, gh, gt), d = pview_row_step(cfg, t, r, (own_ids, hb(own_ids), ts(own_ids)), [sender],
+                                         [(snd_view_ids, hb(snd_view_ids), ts(snd_view_ids))])
+        assert len(gi) == V and np.all(np.diff(gi) > 0)
+        # the sender's own entry is (hb 1, ts t): age 0, alone in the best bin, always kept
+        assert sender in gi
+        tied = np.setdiff1d(np.union1d(own_ids, snd_view_ids), [sender])
+        m = load_oracle().gsp_oracle_draw(0x45564354, seed, t, r, 0, 0) % n if order else 0
+        want = np.sort(tied[np.argsort((tied - m) % n, kind="stable")[:V - 1]])
+        assert np.array_equal(np.setdiff1d(gi, [sender]), want), order
+        assert d["evicts"] == len(tied) - (V - 1)
