@@ -510,14 +510,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
     const uint32_t lo_id = tid > 0 ? key_id(prev_key) + 1u : 0u;   // this lane brackets ids
     const uint32_t hi_id = tid < NT - 1 ? key_id(ck[Q - 1]) : kKeyMax;  // [lo_id, hi_id]
 
-    // res / rid[e]: the lane's surviving entry of key e (0: none).  128-lane rows (kMO): slot Q
-    // takes the shift when the lane's one adopted orphan is inserted in id order (below), so the
-    // survivor passes visit Q + 1 slots instead of Q slots plus an orphan test before each; the
-    // 256-lane rows keep the orphan apart (their one more slot spills at 64 VGPRs)
-    constexpr bool kMO = NT == 128;
-    constexpr int QS = kMO ? Q + 1 : Q;
-    uint32_t res[QS], rid[QS];
-    if constexpr (kMO) res[Q] = rid[Q] = 0;
+    uint32_t res[Q], rid[Q];
     uint32_t nloc = 0, joins = 0, removes = 0, evicts = 0, found_mask = 0;
     uint32_t jmask = 0, rmask = 0;                       // event stream: join / remove keys
     uint32_t hsum = 0;
@@ -632,25 +625,13 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
             if ((adopt >> jj) & 1u) { o_x = ssrc[jj]; o_p = ains[jj]; }
     }
     const bool multi = __ballot(n_orph > 1) != 0ull;          // wave-uniform
-    if (kMO && !multi) {  // the lane's orphan (if any) into res / rid at its id position o_p
-#pragma unroll
-        for (int e = QS - 1; e >= 0; --e) {
-            const bool shift = o_p >= 0 && e > o_p;
-            res[e] = e == o_p ? fresh : shift ? res[e > 0 ? e - 1 : 0] : res[e];
-            rid[e] = e == o_p ? o_x : shift ? rid[e > 0 ? e - 1 : 0] : rid[e];
-        }
-    }
     // rb[e]: the eviction bin of res[e] (filled on the eviction path, computed once per slot)
-    uint32_t rb[QS];
+    uint32_t rb[Q];
 #pragma unroll
-    for (int e = 0; e < QS; ++e) rb[e] = 0;
+    for (int e = 0; e < Q; ++e) rb[e] = 0;
     const uint32_t fresh_bin = pv_bin(fresh, t5, th0);
     auto for_each = [&](auto &&f) {                            // f(value, id, bin)
-        if (kMO && !multi) {
-#pragma unroll
-            for (int e = 0; e < QS; ++e)
-                if (res[e]) f(res[e], rid[e], rb[e]);
-        } else if (!multi) {
+        if (!multi) {
 #pragma unroll
             for (int e = 0; e <= Q; ++e) {
                 if (o_p == e) f(fresh, o_x, fresh_bin);
@@ -683,7 +664,7 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         ro.len = int32_t(total);
     } else {
 #pragma unroll
-        for (int e = 0; e < QS; ++e) rb[e] = pv_bin(res[e], t5, th0);
+        for (int e = 0; e < Q; ++e) rb[e] = pv_bin(res[e], t5, th0);
         for_each([&](uint32_t, uint32_t, uint32_t b) {
             atomicAdd(&bins[b >> 1], 1u << ((b & 1u) * 16u));
         });
@@ -769,19 +750,13 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
                                                : 0u;
         // ties: the boundary bin's entries with hb == hstar (all of them unless e >= 31);
         // plain keeps: lower bins, and boundary-bin entries with a larger hb or without a tie
-        auto count = [&](uint32_t v, uint32_t x, uint32_t b, bool ok) {
+        for_each([&](uint32_t v, uint32_t x, uint32_t b) {
             const uint32_t hb = v >> 5;
-            const bool is_tie = ok && tie && b == bstar && hb == hstar;
+            const bool is_tie = tie && b == bstar && hb == hstar;
             nt += is_tie ? 1u : 0u;
             if (kExt & kExtRot) nth += (is_tie && x >= mrot) ? 1u : 0u;
-            nk += (ok && !is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
-        };
-        if (kMO && !multi) {                                 // predicated, no branches
-#pragma unroll
-            for (int e = 0; e < QS; ++e) count(res[e], rid[e], rb[e], res[e] != 0u);
-        } else {
-            for_each([&](uint32_t v, uint32_t x, uint32_t b) { count(v, x, b, true); });
-        }
+            nk += (!is_tie && (b < bstar || (b == bstar && (!tie || hb > hstar)))) ? 1u : 0u;
+        });
         pm.mark(9);
         uint32_t sums = 0;
         const uint32_t ex = block_scan<NT>(nt | (nk << 16), &sums, scan_buf + 4);
