@@ -27,7 +27,7 @@ HDRS     := $(wildcard $(CSRC)/*.hpp) $(wildcard include/gossip/*.h) $(wildcard 
 all: lib app oracle
 
 lib: $(LIB)
-app: $(APP)
+app: $(APP) $(PKG)/bin/RecvDriver
 
 build:
 	mkdir -p build
@@ -48,6 +48,13 @@ $(LIB): $(OBJS)
 $(APP): $(PKG)/app/app_main.cpp $(LIB) include/gossip/mp1_facade.hpp
 	mkdir -p $(PKG)/bin
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ $(PKG)/app/app_main.cpp \
+	    -L$(PKG) -lgossip_amd -Wl,-rpath,'$$ORIGIN/..'
+
+# test driver of the receive-side entry points (tests/drivers/recv_driver.cpp); the same source
+# is built against the reference under oracle/_ref/RecvDriver
+$(PKG)/bin/RecvDriver: tests/drivers/recv_driver.cpp $(LIB) include/gossip/mp1_facade.hpp
+	mkdir -p $(PKG)/bin
+	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ tests/drivers/recv_driver.cpp \
 	    -L$(PKG) -lgossip_amd -Wl,-rpath,'$$ORIGIN/..'
 
 oracle:

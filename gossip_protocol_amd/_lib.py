@@ -39,6 +39,11 @@ class GspEntry(ctypes.Structure):
                 ("timestamp", c_int64)]
 
 
+class GspQueuedMsg(ctypes.Structure):
+    _fields_ = [("src_id", c_int32), ("type", c_int32), ("send_batch", c_int64),
+                ("payload_off", c_int64), ("payload_len", c_int32), ("pad", c_int32)]
+
+
 class GspExactStats(ctypes.Structure):
     _fields_ = [("batches", c_int64), ("node_rounds", c_int64), ("merges", c_int64),
                 ("draws", c_int64), ("sends_admitted", c_int64), ("device_ms", ctypes.c_double)]
@@ -135,6 +140,12 @@ SIGNATURES = {
     "gsp_get_member": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspMemberView)]),
     "gsp_member_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspEntry), c_int32,
                                        P(c_int32)]),
+    "gsp_payload_snapshots": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
+    "gsp_recv_detach": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, P(GspQueuedMsg), c_int32,
+                                       P(GspEntry), c_int64, P(c_int32), P(c_int64)]),
+    "gsp_queue_push": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspQueuedMsg), P(GspEntry)]),
+    "gsp_recv_callback": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, P(GspQueuedMsg),
+                                         P(GspEntry), c_int32]),
     "gsp_write_msgcount": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, c_int32]),
     "gsp_state_dump": (ctypes.c_int, [ctypes.c_void_p, c_int32, ctypes.c_char_p]),
     "gsp_counters": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), P(c_int32), c_int32]),

@@ -197,6 +197,7 @@ int64_t gsp_struct_size(const char *name) {
     if (s == "gsp_params") return int64_t(sizeof(gsp_params));
     if (s == "gsp_member_view") return int64_t(sizeof(gsp_member_view));
     if (s == "gsp_entry") return int64_t(sizeof(gsp_entry));
+    if (s == "gsp_queued_msg") return int64_t(sizeof(gsp_queued_msg));
     if (s == "gsp_exact_stats") return int64_t(sizeof(gsp_exact_stats));
     if (s == "gsp_fail_event") return int64_t(sizeof(gsp_fail_event));
     if (s == "gsp_policy") return int64_t(sizeof(gsp_policy));

@@ -32,8 +32,20 @@ constexpr int32_t kEnMsgBytes = 16;    // sizeof(en_msg), EmulNet.h:23-30
 
 struct NetMsg {
     int32_t src, dst, type;
-    int64_t send_batch;
+    int64_t send_batch;   // the sender's list version the payload is (its commit batch)
+    int32_t prow = -1;    // >= 0: the payload is pool[prow], a list handed in by the driver
+    int32_t vrow = -1;    // >= 0: the list a driver callback sees is pool[vrow] (a JOINREP's
+                          // list as the reply was sent, MP1Node.cpp:227), not the payload
 };
+
+// A sender's list kept from send time, while messages that carry it are in flight and the
+// sender has committed a newer one (snapshot mode: the driver-side receive paths).
+struct Snapshot {
+    int64_t refs = 0;               // admitted messages carrying this version, not yet consumed
+    bool kept = false;
+    std::vector<gsp_entry> list;
+};
+uint64_t version_key(int32_t src_id, int64_t batch) { return (uint64_t(uint32_t(src_id)) << 40) | uint64_t(batch); }
 
 // strcmp() over the two 6-byte addresses (EmulNet.cpp:154) compares the little-endian id
 // bytes as a C string (the port bytes that follow are 0 for every node), so two ids match
@@ -67,6 +79,13 @@ class EmulBuffer {
     void push(const NetMsg &m) {
         pos_[addr_class(m.dst)].insert(int32_t(msgs_.size()));
         msgs_.push_back(m);
+    }
+    // the messages deliver(id, ...) would take, in the same order, without taking them
+    template <typename F>
+    void peek(int32_t id, F &&see) const {
+        auto it = pos_.find(addr_class(id));
+        if (it == pos_.end()) return;
+        for (auto k = it->second.rbegin(); k != it->second.rend(); ++k) see(msgs_[size_t(*k)]);
     }
     template <typename F>
     void deliver(int32_t id, F &&take) {
@@ -122,6 +141,40 @@ struct gsp_engine {
     bool log_first = true;
 
     gsp_exact_stats stats{};
+
+    // driver-side receive (gsp_recv_detach / gsp_queue_push / gsp_recv_callback)
+    bool snapshots = false;
+    std::unordered_map<uint64_t, Snapshot> versions;   // by version_key(src id, send batch)
+    std::vector<std::vector<gsp_entry>> pool;          // payloads of pushed messages
+    std::vector<int32_t> pool_free;
+    gsp::DevBuf<int64_t> p_key;
+    gsp::DevBuf<int32_t> p_hb, p_ts, p_rank, p_nlist, q_prow;
+    gsp::DevBuf<int64_t> rep_key;
+    gsp::DevBuf<int32_t> rep_hb, rep_ts, rep_off, adm_slot;
+
+    void admitted(int32_t src_id, int64_t batch) {
+        if (snapshots) versions[version_key(src_id, batch)].refs++;
+    }
+    void consumed(const NetMsg &m) {
+        if (m.vrow >= 0) {
+            pool[size_t(m.vrow)].clear();
+            pool_free.push_back(m.vrow);
+        }
+        if (m.prow >= 0) {
+            pool[size_t(m.prow)].clear();
+            pool_free.push_back(m.prow);
+            return;
+        }
+        auto it = versions.find(version_key(m.src, m.send_batch));
+        if (it != versions.end() && --it->second.refs <= 0) versions.erase(it);
+    }
+    int32_t pool_put(std::vector<gsp_entry> &&list) {
+        int32_t k;
+        if (!pool_free.empty()) { k = pool_free.back(); pool_free.pop_back(); }
+        else { k = int32_t(pool.size()); pool.emplace_back(); }
+        pool[size_t(k)] = std::move(list);
+        return k;
+    }
 
     // device
     gsp::DevBuf<int64_t> t_key, o_key, d_ev_raw;
@@ -203,6 +256,83 @@ int check_engine(gsp_engine *e) {
     return GSP_OK;
 }
 
+// `node`'s committed member list in list order (one device read).
+int read_list(gsp_engine *e, int32_t node, std::vector<gsp_entry> &list) {
+    const int32_t N = e->n;
+    std::vector<int64_t> key(N);
+    std::vector<int32_t> hb(N), ts(N), rank(N);
+    const size_t row = size_t(node) * N;
+    GSP_HIP(hipMemcpyAsync(key.data(), e->t_key.p + row, N * 8, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(hb.data(), e->t_hb.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(ts.data(), e->t_ts.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(rank.data(), e->t_rank.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    list.assign(size_t(N), gsp_entry{});
+    int32_t cnt = 0;
+    for (int32_t x = 0; x < N; ++x) {
+        if (key[x] < 0) continue;
+        GSP_REQUIRE(rank[x] >= 0 && rank[x] < N, GSP_ERR_INVALID, "corrupt rank");
+        list[size_t(rank[x])] = gsp_entry{x + 1, 0, hb[x], ts[x]};
+        cnt++;
+    }
+    list.resize(size_t(cnt));
+    return GSP_OK;
+}
+
+// The payload of a queued message (the sender's list at send time, MP1Node.cpp:138/227/357):
+// *out = its pool list or the list kept from send time, or nullptr when it is the sender's
+// committed row (the sender has not committed since the send).
+int payload_of(gsp_engine *e, const NetMsg &m, const std::vector<gsp_entry> **out) {
+    *out = nullptr;
+    if (m.prow >= 0) {
+        *out = &e->pool[size_t(m.prow)];
+        return GSP_OK;
+    }
+    const int32_t s = m.src - 1;
+    GSP_REQUIRE(s >= 0 && s < e->n, GSP_ERR_INVALID, "message from id %d", m.src);
+    if (e->last_commit[s] == m.send_batch) return GSP_OK;
+    auto it = e->versions.find(version_key(m.src, m.send_batch));
+    GSP_REQUIRE(it != e->versions.end() && it->second.kept, GSP_ERR_ORDER,
+                "message from id %d to id %d has a stale payload (sender re-processed since the "
+                "send; gsp_payload_snapshots keeps send-time lists)", m.src, m.dst);
+    *out = &it->second.list;
+    return GSP_OK;
+}
+
+// A driver-built payload: ids 1..N, port 0, each id once (one table column per id).
+int check_payload(const gsp_engine *e, const gsp_entry *p, int32_t n) {
+    GSP_REQUIRE(n >= 0 && n <= e->n && (p || n == 0), GSP_ERR_INVALID,
+                "payload of %d entries (at most %d)", n, e->n);
+    std::vector<int8_t> seen(size_t(e->n), 0);
+    for (int32_t i = 0; i < n; ++i) {
+        GSP_REQUIRE(p[i].id >= 1 && p[i].id <= e->n && p[i].port == 0, GSP_ERR_INVALID,
+                    "payload entry %d: id %d port %d (ids 1..%d, port 0)", i, p[i].id,
+                    int(p[i].port), e->n);
+        GSP_REQUIRE(!seen[size_t(p[i].id - 1)], GSP_ERR_INVALID, "payload entry %d: id %d twice",
+                    i, p[i].id);
+        GSP_REQUIRE(p[i].heartbeat >= INT32_MIN && p[i].heartbeat <= INT32_MAX &&
+                    p[i].timestamp >= INT32_MIN && p[i].timestamp <= INT32_MAX,
+                    GSP_ERR_INVALID, "payload entry %d: heartbeat/timestamp outside int32", i);
+        seen[size_t(p[i].id - 1)] = 1;
+    }
+    return GSP_OK;
+}
+
+int make_msg(gsp_engine *e, int32_t node, const gsp_queued_msg *m, const gsp_entry *payload,
+             NetMsg *out) {
+    GSP_REQUIRE(m && node >= 0 && node < e->n, GSP_ERR_INVALID, "bad message or node %d", node);
+    GSP_REQUIRE(m->src_id >= 1 && m->src_id <= e->n, GSP_ERR_INVALID, "message from id %d",
+                m->src_id);
+    GSP_REQUIRE(m->type == GSP_MSG_JOINREQ || m->type == GSP_MSG_JOINREP ||
+                m->type == GSP_MSG_GOSSIP, GSP_ERR_INVALID, "message type %d", m->type);
+    *out = NetMsg{m->src_id, node + 1, m->type, m->send_batch};
+    if (payload) {
+        if (int rc = check_payload(e, payload, m->payload_len)) return rc;
+        out->prow = e->pool_put(std::vector<gsp_entry>(payload, payload + m->payload_len));
+    }
+    return GSP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -281,9 +411,13 @@ int gsp_destroy(gsp_engine *e) {
     for (auto *b : {&e->t_hb, &e->t_ts, &e->t_rank, &e->t_state, &e->o_hb, &e->o_ts, &e->o_rank,
                     &e->o_state, &e->b_node, &e->b_op, &e->q_off, &e->q_src, &e->q_type,
                     &e->send_off, &e->send_dst, &e->send_type, &e->send_cnt, &e->counters,
-                    &e->stream, &e->adm_src, &e->adm_dst, &e->adm_type, &e->sent_ctr})
+                    &e->stream, &e->adm_src, &e->adm_dst, &e->adm_type, &e->sent_ctr, &e->p_hb,
+                    &e->p_ts, &e->p_rank, &e->p_nlist, &e->q_prow, &e->rep_hb, &e->rep_ts,
+                    &e->rep_off, &e->adm_slot})
         b->release();
     e->t_key.release();
+    e->p_key.release();
+    e->rep_key.release();
     e->o_key.release();
     e->events.release();
     e->merges.release();
@@ -320,7 +454,39 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     GSP_REQUIRE(n <= N, GSP_ERR_INVALID, "gsp_tick_process: batch of %d > %d nodes", n, N);
     std::vector<int8_t> seen(N, 0);
     std::vector<int32_t> h_node(n), h_op(n), h_qoff(n + 1, 0), h_soff(n + 1, 0);
-    std::vector<int32_t> h_qsrc, h_qtype;
+    std::vector<int32_t> h_repoff(n + 1, 0);   // JOINREP list rows of each batch position
+    std::vector<int32_t> h_qsrc, h_qtype, h_qprow;
+    // payload rows of messages whose list is not the sender's committed row
+    std::vector<int64_t> hp_key;
+    std::vector<int32_t> hp_hb, hp_ts, hp_rank, hp_nlist;
+    auto stage = [&](const std::vector<gsp_entry> &list) {
+        const size_t base = hp_nlist.size() * size_t(N);
+        hp_key.resize(base + N, -1);
+        hp_hb.resize(base + N, 0);
+        hp_ts.resize(base + N, 0);
+        hp_rank.resize(base + N, -1);
+        for (size_t i = 0; i < list.size(); ++i) {
+            const size_t o = base + size_t(list[i].id - 1);
+            hp_key[o] = 0;
+            hp_hb[o] = int32_t(list[i].heartbeat);
+            hp_ts[o] = int32_t(list[i].timestamp);
+            hp_rank[o] = int32_t(i);
+        }
+        hp_nlist.push_back(int32_t(list.size()));
+        return int32_t(hp_nlist.size()) - 1;
+    };
+    if (e->snapshots) {
+        // keep the lists in-flight messages carry before this batch commits newer ones
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t node = order[i];
+            if (node < 0 || node >= N) continue;   // rejected below
+            auto it = e->versions.find(version_key(node + 1, e->last_commit[node]));
+            if (it != e->versions.end() && it->second.refs > 0 && !it->second.kept) {
+                if (int rc = read_list(e, node, it->second.list)) return rc;
+                it->second.kept = true;
+            }
+        }
+    }
     for (int32_t i = 0; i < n; ++i) {
         const int32_t node = order[i];
         const int32_t op = ops[i];
@@ -334,26 +500,28 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         h_op[i] = op;
         int32_t njreq = 0;
         if (op == GSP_OP_LOOP || op == GSP_OP_CHECK) {
+            GSP_REQUIRE(e->queue[node].size() < (1u << 20), GSP_ERR_CAPACITY,
+                        "gsp_tick_process: queue of node %d too long", node);
             for (const NetMsg &m : e->queue[node]) {
+                int32_t prow = -1;
                 if (m.type == GSP_MSG_GOSSIP || (m.type == GSP_MSG_JOINREP && e->p.intro_list > 0)) {
-                    const int32_t s = m.src - 1;
-                    // the payload is the sender's list at send time (MP1Node.cpp:357); the
-                    // device reads it from the committed table, so it must be unchanged
-                    GSP_REQUIRE(s >= 0 && s < N && e->last_commit[s] == m.send_batch,
-                                GSP_ERR_ORDER,
-                                "gsp_tick_process: GOSSIP from id %d to node %d has a stale "
-                                "payload (sender re-processed since the send)", m.src, node);
+                    // the payload is the sender's list at send time (MP1Node.cpp:357): its
+                    // committed row while unchanged, else a kept or driver-handed list
+                    const std::vector<gsp_entry> *pl = nullptr;
+                    if (int rc = payload_of(e, m, &pl)) return rc;
+                    if (pl) prow = stage(*pl);
                 }
                 njreq += m.type == GSP_MSG_JOINREQ;
                 h_qsrc.push_back(m.src);
                 h_qtype.push_back(m.type);
+                h_qprow.push_back(prow);
             }
-            GSP_REQUIRE(e->queue[node].size() < (1u << 20), GSP_ERR_CAPACITY,
-                        "gsp_tick_process: queue of node %d too long", node);
+            for (const NetMsg &m : e->queue[node]) e->consumed(m);
             e->queue[node].clear();
         }
         h_qoff[i + 1] = int32_t(h_qsrc.size());
         h_soff[i + 1] = h_soff[i] + njreq + 1 + N;
+        h_repoff[i + 1] = h_repoff[i] + (op == GSP_OP_START ? 0 : njreq);
     }
     const int32_t send_cap = h_soff[n];
     hipStream_t st = e->st;
@@ -361,6 +529,24 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         upload_i32(e->q_off, h_qoff, st) || upload_i32(e->q_src, h_qsrc, st) ||
         upload_i32(e->q_type, h_qtype, st) || upload_i32(e->send_off, h_soff, st))
         return GSP_ERR_HIP;
+    const bool staged = !hp_nlist.empty();
+    if (staged) {
+        GSP_HIP(e->p_key.alloc(hp_key.size()));
+        GSP_HIP(hipMemcpyAsync(e->p_key.p, hp_key.data(), hp_key.size() * 8, hipMemcpyHostToDevice, st));
+        if (upload_i32(e->p_hb, hp_hb, st) || upload_i32(e->p_ts, hp_ts, st) ||
+            upload_i32(e->p_rank, hp_rank, st) || upload_i32(e->p_nlist, hp_nlist, st) ||
+            upload_i32(e->q_prow, h_qprow, st))
+            return GSP_ERR_HIP;
+    }
+    // snapshot mode: the list each JOINREP carries as it is sent, for driver callbacks
+    const int32_t n_rep = e->snapshots ? h_repoff[n] : 0;
+    if (n_rep) {
+        GSP_HIP(e->rep_key.alloc(size_t(n_rep) * N));
+        GSP_HIP(e->rep_hb.alloc(size_t(n_rep) * N));
+        GSP_HIP(e->rep_ts.alloc(size_t(n_rep) * N));
+        GSP_HIP(e->adm_slot.alloc(send_cap));
+        if (upload_i32(e->rep_off, h_repoff, st)) return GSP_ERR_HIP;
+    }
     GSP_HIP(e->send_dst.alloc(send_cap));
     GSP_HIP(e->send_type.alloc(send_cap));
     GSP_HIP(e->send_cnt.alloc(n));
@@ -381,6 +567,13 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     b.n_batch = n;
     b.node = e->b_node.p; b.op = e->b_op.p;
     b.q_off = e->q_off.p; b.q_src = e->q_src.p; b.q_type = e->q_type.p;
+    b.q_prow = staged ? e->q_prow.p : nullptr;
+    b.p_key = e->p_key.p; b.p_hb = e->p_hb.p; b.p_ts = e->p_ts.p; b.p_rank = e->p_rank.p;
+    b.p_nlist = e->p_nlist.p;
+    b.rep_off = e->rep_off.p;
+    b.rep_key = n_rep ? e->rep_key.p : nullptr;
+    b.rep_hb = e->rep_hb.p;
+    b.rep_ts = e->rep_ts.p;
     b.send_off = e->send_off.p;
     b.o_key = e->o_key.p; b.o_hb = e->o_hb.p; b.o_ts = e->o_ts.p; b.o_rank = e->o_rank.p;
     b.o_state = e->o_state.p;
@@ -395,6 +588,7 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     s.node = e->b_node.p; s.send_off = e->send_off.p; s.send_cnt = e->send_cnt.p;
     s.send_dst = e->send_dst.p; s.send_type = e->send_type.p;
     s.rng_mode = e->rng_mode;
+    s.adm_slot = n_rep ? e->adm_slot.p : nullptr;
     s.glibc_stream = e->stream.p;
     s.stream_base = e->draws;
     s.g0 = e->draws;
@@ -438,6 +632,18 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         GSP_HIP(hipMemcpyAsync(a_dst.data(), e->adm_dst.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
         GSP_HIP(hipMemcpyAsync(a_type.data(), e->adm_type.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
     }
+    std::vector<int64_t> r_key;
+    std::vector<int32_t> r_hb, r_ts, a_slot;
+    if (n_rep && n_adm) {
+        r_key.resize(size_t(n_rep) * N);
+        r_hb.resize(r_key.size());
+        r_ts.resize(r_key.size());
+        a_slot.resize(size_t(n_adm));
+        GSP_HIP(hipMemcpyAsync(r_key.data(), e->rep_key.p, r_key.size() * 8, hipMemcpyDeviceToHost, st));
+        GSP_HIP(hipMemcpyAsync(r_hb.data(), e->rep_hb.p, r_hb.size() * 4, hipMemcpyDeviceToHost, st));
+        GSP_HIP(hipMemcpyAsync(r_ts.data(), e->rep_ts.p, r_ts.size() * 4, hipMemcpyDeviceToHost, st));
+        GSP_HIP(hipMemcpyAsync(a_slot.data(), e->adm_slot.p, size_t(n_adm) * 4, hipMemcpyDeviceToHost, st));
+    }
     GSP_HIP(hipStreamSynchronize(st));
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->stats.device_ms += ms;
@@ -460,8 +666,25 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
             default: e->member_line(node, tick, x.subject, "removed"); break;
         }
     }
-    for (int32_t k = 0; k < n_adm; ++k)
-        e->buf.push(NetMsg{a_src[k], a_dst[k], a_type[k], e->batch_seq});
+    for (int32_t k = 0; k < n_adm; ++k) {
+        NetMsg m{a_src[k], a_dst[k], a_type[k], e->batch_seq};
+        if (!a_slot.empty() && a_type[k] == GSP_MSG_JOINREP) {
+            // replies lead each node's send list: slot - send_off[pos] is the reply index
+            const int32_t pos = int32_t(std::upper_bound(h_soff.begin(), h_soff.end(), a_slot[k]) -
+                                        h_soff.begin()) - 1;
+            const size_t row = size_t(h_repoff[pos] + a_slot[k] - h_soff[pos]) * N;
+            std::vector<std::pair<int64_t, int32_t>> cols;
+            for (int32_t x = 0; x < N; ++x)
+                if (r_key[row + x] >= 0) cols.emplace_back(r_key[row + x], x);
+            std::sort(cols.begin(), cols.end());
+            std::vector<gsp_entry> list;
+            for (const auto &c : cols)
+                list.push_back(gsp_entry{c.second + 1, 0, r_hb[row + c.second], r_ts[row + c.second]});
+            m.vrow = e->pool_put(std::move(list));
+        }
+        e->buf.push(m);
+        e->admitted(a_src[k], e->batch_seq);
+    }
     for (int32_t i = 0; i < n; ++i) {
         const int32_t node = h_node[i];
         e->inited[node] = o_state[size_t(i) * 4 + 0];
@@ -480,6 +703,89 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
     e->stats.merges = int64_t(merges);
     e->batch_seq++;
     return GSP_OK;
+}
+
+int gsp_payload_snapshots(gsp_engine *e, int32_t on) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "gsp_payload_snapshots: NULL engine");
+    e->snapshots = on != 0;
+    if (!e->snapshots) e->versions.clear();
+    return GSP_OK;
+}
+
+int gsp_recv_detach(gsp_engine *e, int32_t tick, int32_t node, gsp_queued_msg *msgs, int32_t cap,
+                    gsp_entry *payload, int64_t payload_cap, int32_t *n, int64_t *n_payload) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(n && n_payload && node >= 0 && node < e->n, GSP_ERR_INVALID,
+                "gsp_recv_detach: bad argument");
+    GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_recv_detach: tick %d", tick);
+    const int32_t id = node + 1;
+    int32_t cnt = 0;
+    int64_t total = 0;
+    int rc = GSP_OK;
+    e->buf.peek(id, [&](const NetMsg &m) {
+        const std::vector<gsp_entry> *pl = m.vrow >= 0 ? &e->pool[size_t(m.vrow)] : nullptr;
+        if (rc == GSP_OK && !pl) rc = payload_of(e, m, &pl);
+        cnt++;
+        total += pl ? int64_t(pl->size()) : int64_t(e->nlist[size_t(m.src - 1)]);
+    });
+    if (rc) return rc;
+    *n = cnt;
+    *n_payload = total;
+    if (!msgs) return GSP_OK;                                 // sizes only, nothing taken
+    GSP_REQUIRE(cap >= cnt && payload_cap >= total && (payload || total == 0), GSP_ERR_CAPACITY,
+                "gsp_recv_detach: %d messages / %lld payload entries do not fit %d / %lld", cnt,
+                (long long)total, cap, (long long)payload_cap);
+    std::unordered_map<int32_t, std::vector<gsp_entry>> live;   // committed rows read here
+    int32_t k = 0;
+    int64_t off = 0;
+    e->buf.deliver(id, [&](const NetMsg &m) {                 // EmulNet.cpp:151-173
+        e->recv_ctr[size_t(id) * kMaxTicks + tick]++;
+        const std::vector<gsp_entry> *pl = m.vrow >= 0 ? &e->pool[size_t(m.vrow)] : nullptr;
+        if (rc == GSP_OK && !pl) rc = payload_of(e, m, &pl);
+        if (rc == GSP_OK && !pl) {
+            auto it = live.find(m.src);
+            if (it == live.end()) {
+                it = live.emplace(m.src, std::vector<gsp_entry>()).first;
+                rc = read_list(e, m.src - 1, it->second);
+            }
+            pl = &it->second;
+        }
+        gsp_queued_msg &q = msgs[k++];
+        q.src_id = m.src;
+        q.type = m.type;
+        q.send_batch = m.send_batch;
+        q.payload_off = off;
+        q.payload_len = pl && rc == GSP_OK ? int32_t(pl->size()) : 0;
+        if (q.payload_len) std::memcpy(payload + off, pl->data(), pl->size() * sizeof(gsp_entry));
+        off += q.payload_len;
+        e->consumed(m);
+    });
+    return rc;
+}
+
+int gsp_queue_push(gsp_engine *e, int32_t node, const gsp_queued_msg *m, const gsp_entry *payload) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "gsp_queue_push: NULL engine");
+    NetMsg nm;
+    if (int rc = make_msg(e, node, m, payload, &nm)) return rc;
+    e->queue[size_t(node)].push_back(nm);
+    return GSP_OK;
+}
+
+int gsp_recv_callback(gsp_engine *e, int32_t tick, int32_t node, const gsp_queued_msg *m,
+                      const gsp_entry *payload, int32_t dropmsg) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "gsp_recv_callback: NULL engine");
+    NetMsg nm;
+    if (int rc = make_msg(e, node, m, payload, &nm)) return rc;
+    // exactly this message, now: a CHECK batch over a one-message queue; the node's own queue
+    // is set aside and comes back unchanged
+    std::vector<NetMsg> held;
+    held.swap(e->queue[size_t(node)]);
+    e->queue[size_t(node)].push_back(nm);
+    const int8_t op = GSP_OP_CHECK;
+    const int rc = gsp_tick_process(e, tick, &node, &op, 1, dropmsg);
+    if (rc && !e->queue[size_t(node)].empty()) e->consumed(e->queue[size_t(node)].front());
+    e->queue[size_t(node)].swap(held);
+    return rc;
 }
 
 int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
@@ -506,6 +812,7 @@ int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int3
         return GSP_OK;
     // the payload of a GOSSIP is the sender's list as committed now
     e->buf.push(NetMsg{src_id, dst_id, type, e->last_commit[src_node]});
+    e->admitted(src_id, e->last_commit[src_node]);
     e->sent_host[size_t(src_id) * kMaxTicks + tick]++;
     e->stats.sends_admitted++;
     *admitted = kMsgHdrBytes;
@@ -553,25 +860,10 @@ int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, in
     if (int rc = check_engine(e)) return rc;
     GSP_REQUIRE(node >= 0 && node < e->n && n && (buf || cap == 0), GSP_ERR_INVALID,
                 "gsp_member_list: bad argument");
-    const int32_t N = e->n;
-    std::vector<int64_t> key(N);
-    std::vector<int32_t> hb(N), ts(N), rank(N);
-    const size_t row = size_t(node) * N;
-    GSP_HIP(hipMemcpyAsync(key.data(), e->t_key.p + row, N * 8, hipMemcpyDeviceToHost, e->st));
-    GSP_HIP(hipMemcpyAsync(hb.data(), e->t_hb.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
-    GSP_HIP(hipMemcpyAsync(ts.data(), e->t_ts.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
-    GSP_HIP(hipMemcpyAsync(rank.data(), e->t_rank.p + row, N * 4, hipMemcpyDeviceToHost, e->st));
-    GSP_HIP(hipStreamSynchronize(e->st));
-    std::vector<gsp_entry> list(N);
-    int32_t cnt = 0;
-    for (int32_t x = 0; x < N; ++x) {
-        if (key[x] < 0) continue;
-        GSP_REQUIRE(rank[x] >= 0 && rank[x] < N, GSP_ERR_INVALID, "corrupt rank");
-        list[rank[x]] = gsp_entry{x + 1, 0, hb[x], ts[x]};
-        cnt++;
-    }
-    *n = cnt;
-    for (int32_t k = 0; k < cnt && k < cap; ++k) buf[k] = list[k];
+    std::vector<gsp_entry> list;
+    if (int rc = read_list(e, node, list)) return rc;
+    *n = int32_t(list.size());
+    for (int32_t k = 0; k < *n && k < cap; ++k) buf[k] = list[size_t(k)];
     return GSP_OK;
 }
 

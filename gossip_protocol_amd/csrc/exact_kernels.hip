@@ -33,6 +33,21 @@ __device__ inline void push_event(const ExactBatchDev &b, int32_t pos, int32_t k
     }
 }
 
+// Where a queued message's payload list lives: the sender's committed row, or a row of the
+// payload arrays (a list the driver handed in, or the sender's list kept from send time).
+struct Payload {
+    const int64_t *key;
+    const int32_t *hb, *ts, *rank;
+    size_t row;
+    int32_t nlist;
+};
+__device__ inline Payload payload_of(const ExactTable &tab, const ExactBatchDev &b, int32_t q,
+                                     int32_t sc, int32_t n) {
+    const int32_t pr = b.q_prow ? b.q_prow[q] : -1;
+    if (pr >= 0) return Payload{b.p_key, b.p_hb, b.p_ts, b.p_rank, size_t(pr) * n, b.p_nlist[pr]};
+    return Payload{tab.key, tab.hb, tab.ts, tab.rank, size_t(sc) * n, tab.nlist[sc]};
+}
+
 __global__ void __launch_bounds__(kMaxBlock)
 exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int64_t batch_seq,
                    int32_t tremove, int32_t id_filter_limit) {
@@ -89,6 +104,12 @@ exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int
                     push_event(b, pos, kEvJoin, x, (int64_t(j) << 20));
                 }
                 if (type == 0) {                   // reply JOINREP in queue order
+                    if (b.rep_key && valid) {
+                        const size_t o = size_t(b.rep_off[pos] + n_replies) * n + x;
+                        b.rep_key[o] = present ? key : -1;
+                        b.rep_hb[o] = hb;
+                        b.rep_ts[o] = ts;
+                    }
                     if (x == 0) {
                         b.send_dst[sbase + n_replies] = sid;
                         b.send_type[sbase + n_replies] = 1;
@@ -97,26 +118,27 @@ exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int
                 } else {
                     in_group = 1;
                     if (b.intro_list > 0 && valid && x != sc) {   // opt-in bounded introducer list
-                        const size_t srow = size_t(sc) * n;
-                        const int32_t cnt = tab.nlist[sc];
+                        const Payload pl = payload_of(tab, b, q, sc, n);
+                        const size_t srow = pl.row;
+                        const int32_t cnt = pl.nlist;
                         const int32_t B = b.intro_list < cnt ? b.intro_list : cnt;
                         int32_t ranks[16];
                         int32_t nch = 0;
                         for (int32_t i = 0; i < B; ++i)
                             next_distinct_rank(draw_u31(kDomainJoin, b.seed, uint32_t(tick - 1), 0u,
                                                         uint32_t(r), uint32_t(i)), cnt, i, ranks, nch);
-                        const int64_t kv = tab.key[srow + x];
+                        const int64_t kv = pl.key[srow + x];
                         bool chosen = false;
                         if (kv >= 0)
-                            for (int32_t i = 0; i < nch; ++i) chosen = chosen || ranks[i] == tab.rank[srow + x];
+                            for (int32_t i = 0; i < nch; ++i) chosen = chosen || ranks[i] == pl.rank[srow + x];
                         // the GOSSIP payload rules (MP1Node.cpp:244-258), filter included
                         if (chosen && x + 1 < id_filter_limit) {
-                            const int32_t hv = tab.hb[srow + x];
-                            const int32_t tv = tab.ts[srow + x];
+                            const int32_t hv = pl.hb[srow + x];
+                            const int32_t tv = pl.ts[srow + x];
                             if (present) {
                                 if (hv > hb) { hb = hv; ts = tick; }
                             } else if (x != r && tick - tv < tremove) {
-                                const int32_t p1 = tab.rank[srow + x] + 1;
+                                const int32_t p1 = pl.rank[srow + x] + 1;
                                 present = true; hb = hv; ts = tv;
                                 key = make_key(batch_seq, j, p1);
                                 push_event(b, pos, kEvJoin, x, (int64_t(j) << 20) | p1);
@@ -125,7 +147,8 @@ exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int
                     }
                 }
             } else if (type == 3) {                // GOSSIP
-                merges += 1ull + uint64_t(tab.nlist[sc]);
+                const Payload pl = payload_of(tab, b, q, sc, n);
+                merges += 1ull + uint64_t(pl.nlist);
                 if (x == sc) {
                     if (present) { hb += 1; ts = tick; }
                     else {
@@ -133,17 +156,24 @@ exact_batch_kernel(ExactTable tab, ExactBatchDev b, int32_t n, int32_t tick, int
                         key = make_key(batch_seq, j, 0);
                         push_event(b, pos, kEvJoin, x, (int64_t(j) << 20));
                     }
+                    // the sender's own entry in its payload (never in a committed row: a list
+                    // does not hold its owner; a driver-built list may), MP1Node.cpp:246-251
+                    if (valid && pl.key[pl.row + x] >= 0 && x + 1 < id_filter_limit &&
+                        pl.hb[pl.row + x] > hb) {
+                        hb = pl.hb[pl.row + x];
+                        ts = tick;
+                    }
                 } else if (valid) {
-                    const size_t srow = size_t(sc) * n;
-                    const int64_t kv = tab.key[srow + x];
+                    const size_t srow = pl.row;
+                    const int64_t kv = pl.key[srow + x];
                     // payload filter 0 <= id < 10 (MP1Node.cpp:245); id = x + 1
                     if (kv >= 0 && x + 1 >= 0 && x + 1 < id_filter_limit) {
-                        const int32_t hv = tab.hb[srow + x];
-                        const int32_t tv = tab.ts[srow + x];
+                        const int32_t hv = pl.hb[srow + x];
+                        const int32_t tv = pl.ts[srow + x];
                         if (present) {
                             if (hv > hb) { hb = hv; ts = tick; }
                         } else if (x != r && tick - tv < tremove) {
-                            const int32_t p1 = tab.rank[srow + x] + 1;
+                            const int32_t p1 = pl.rank[srow + x] + 1;
                             present = true; hb = hv; ts = tv;
                             key = make_key(batch_seq, j, p1);
                             push_event(b, pos, kEvJoin, x, (int64_t(j) << 20) | p1);
@@ -276,7 +306,7 @@ __global__ void __launch_bounds__(kMaxBlock) exact_send_kernel(ExactSendDev s) {
     // 2. per send: draw, drop, admission (first buff_room survivors), compaction
     for (int32_t c0 = 0; c0 < total; c0 += blockDim.x) {
         const int32_t i = c0 + tid;
-        int32_t src = 0, dst = 0, type = 0, keep = 0;
+        int32_t src = 0, dst = 0, type = 0, keep = 0, slot = 0;
         if (i < total) {
             int32_t lo = 0, hi = s.n_batch - 1;   // batch node owning send i
             while (lo < hi) {
@@ -285,8 +315,9 @@ __global__ void __launch_bounds__(kMaxBlock) exact_send_kernel(ExactSendDev s) {
             }
             const int32_t k = i - s_base[lo];
             src = s.node[lo] + 1;
-            dst = s.send_dst[s.send_off[lo] + k];
-            type = s.send_type[s.send_off[lo] + k];
+            slot = s.send_off[lo] + k;
+            dst = s.send_dst[slot];
+            type = s.send_type[slot];
             const int64_t g = s.g0 + i;
             int32_t draw;
             if (s.rng_mode == 1)
@@ -303,6 +334,7 @@ __global__ void __launch_bounds__(kMaxBlock) exact_send_kernel(ExactSendDev s) {
             s.adm_src[before] = src;
             s.adm_dst[before] = dst;
             s.adm_type[before] = type;
+            if (s.adm_slot) s.adm_slot[before] = slot;
             atomicAdd(&s.sent_ctr[size_t(src) * s.max_ticks + s.tick], 1);
         }
         __syncthreads();

@@ -35,6 +35,20 @@ struct ExactBatchDev {
     const int32_t *node, *op;          // [B]
     const int32_t *q_off;              // [B+1] CSR of each node's drained queue
     const int32_t *q_src, *q_type;     // [Q]  sender id, message type
+    // payload of each queued message: q_prow[q] < 0 reads the sender's committed row of the
+    // table (the normal case), >= 0 the row q_prow[q] of the p_* arrays, a list handed in by
+    // the driver or kept from send time (gsp_queue_push / gsp_recv_callback / snapshots);
+    // q_prow null: every payload is a committed row
+    const int32_t *q_prow;             // [Q] or null
+    const int64_t *p_key;              // [P][N] >= 0 present
+    const int32_t *p_hb, *p_ts, *p_rank;   // [P][N]
+    const int32_t *p_nlist;            // [P]
+    // the list each JOINREP carries, as the reply is sent (MP1Node.cpp:225-229: after the
+    // JOINREQ's addMember, before the rest of the queue): row rep_off[pos] + (reply index),
+    // columns key (>= 0 present, list order) / hb / ts; rep_key null: not recorded
+    const int32_t *rep_off;            // [B]
+    int64_t *rep_key;
+    int32_t *rep_hb, *rep_ts;
     const int32_t *send_off;           // [B+1] capacity offsets of the per-node send lists
     // outputs
     int64_t *o_key;                    // [B][N]
@@ -56,6 +70,7 @@ struct ExactSendDev {
     int32_t n_batch;
     const int32_t *node, *send_off, *send_cnt, *send_dst, *send_type;
     int32_t rng_mode;                  // 0 glibc stream, 1 philox
+    int32_t *adm_slot;                 // [admitted] send-list slot (send_off[pos] + k), or null
     const int32_t *glibc_stream;       // values of rand() by draw index
     int64_t stream_base;               // draw index of glibc_stream[0]
     int64_t g0;                        // global draw index of the batch's first send

@@ -88,6 +88,59 @@ class Engine:
         check(lib().gsp_log_bytes(self._h, buf, n.value, ctypes.byref(n)), "gsp_log_bytes")
         return buf.raw[:n.value]
 
+    # driver-side receive (gossip.h): ENrecv with a driver callback, Queue::enqueue, direct
+    # recvCallBack; a message is (src_id, type, send_batch, [(id, heartbeat, timestamp), ...])
+    def payload_snapshots(self, on=True):
+        check(lib().gsp_payload_snapshots(self._h, int(on)), "gsp_payload_snapshots")
+
+    def detach_sizes(self, tick, node):
+        n, np_ = ctypes.c_int32(), ctypes.c_int64()
+        check(lib().gsp_recv_detach(self._h, tick, node, None, 0, None, 0, ctypes.byref(n),
+                                    ctypes.byref(np_)), "gsp_recv_detach")
+        return n.value, np_.value
+
+    def detach(self, tick, node):
+        cnt, total = self.detach_sizes(tick, node)
+        msgs = (_lib.GspQueuedMsg * max(1, cnt))()
+        pl = (_lib.GspEntry * max(1, total))()
+        n, np_ = ctypes.c_int32(), ctypes.c_int64()
+        check(lib().gsp_recv_detach(self._h, tick, node, msgs, cnt, pl, total, ctypes.byref(n),
+                                    ctypes.byref(np_)), "gsp_recv_detach")
+        out = []
+        for m in msgs[:n.value]:
+            ents = [(pl[k].id, pl[k].heartbeat, pl[k].timestamp)
+                    for k in range(m.payload_off, m.payload_off + m.payload_len)]
+            out.append((m.src_id, m.type, m.send_batch, ents))
+        return out
+
+    @staticmethod
+    def _msg(src_id, type_, payload, send_batch=-1):
+        m = _lib.GspQueuedMsg(src_id=src_id, type=type_, send_batch=send_batch)
+        if payload is None:
+            return m, None
+        m.payload_len = len(payload)
+        arr = (_lib.GspEntry * max(1, len(payload)))()
+        for k, ent in enumerate(payload):
+            ident, hb, ts = ent[:3]
+            arr[k] = _lib.GspEntry(id=ident, port=ent[3] if len(ent) > 3 else 0, heartbeat=hb,
+                                   timestamp=ts)
+        return m, arr
+
+    def queue_push(self, node, src_id, type_, payload, send_batch=-1):
+        m, arr = self._msg(src_id, type_, payload, send_batch)
+        return lib().gsp_queue_push(self._h, node, ctypes.byref(m), arr)
+
+    def recv_callback(self, tick, node, src_id, type_, payload, dropmsg=0, send_batch=-1):
+        m, arr = self._msg(src_id, type_, payload, send_batch)
+        return lib().gsp_recv_callback(self._h, tick, node, ctypes.byref(m), arr, int(dropmsg))
+
+    def counters(self, ticks):
+        n = self.n + 1
+        sent = (ctypes.c_int32 * (n * ticks))()
+        recv = (ctypes.c_int32 * (n * ticks))()
+        check(lib().gsp_counters(self._h, sent, recv, ticks), "gsp_counters")
+        return list(sent), list(recv)
+
     def stats(self):
         s = _lib.GspExactStats()
         check(lib().gsp_exact_stats_get(self._h, ctypes.byref(s)), "gsp_exact_stats_get")

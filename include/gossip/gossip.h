@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 4
+#define GSP_ABI_VERSION 5
 
 typedef enum {
     GSP_OK = 0,
@@ -168,6 +168,48 @@ int gsp_set_failed(gsp_engine *e, int32_t node, int32_t failed);
 int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out);
 /* The member list of `node` in list order (MemberListEntry vector order). */
 int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n);
+
+/* ---- Driver-side receive: EmulNet::ENrecv with the driver's own callback and direct
+ * MP1Node::recvCallBack calls (MP1Node.cpp:46, 209, 219).  The reference hands the callback
+ * each message as a MessageHdr whose vector_list is the sender's list at send time
+ * (MP1Node.cpp:138/227/357); these calls move such messages between the engine and the
+ * driver with that list attached, so a driver can observe, drop, reorder, hold back or
+ * rewrite messages and process them one at a time.  mp1_facade.hpp builds the reference's
+ * ENrecv / recvCallBack / checkMessages on them. */
+typedef struct {
+    int32_t src_id;       /* the sender's address id (MessageHdr::addr)                    */
+    int32_t type;         /* gsp_msg_type (MessageHdr::msgType)                            */
+    int64_t send_batch;   /* engine-side payload version (opaque to the driver)            */
+    int64_t payload_off;  /* gsp_recv_detach: first entry of the payload in `payload`      */
+    int32_t payload_len;  /* payload entries (MessageHdr::vector_list.size())              */
+    int32_t pad;
+} gsp_queued_msg;
+
+/* Keep each sender's send-time list while messages carry it and the sender commits a newer
+ * one (off by default: the batched phases never need it).  Needed once messages can be
+ * processed in separate batches (gsp_recv_callback), so the facade turns it on at the first
+ * driver-callback receive. */
+int gsp_payload_snapshots(gsp_engine *e, int32_t on);
+
+/* EmulNet::ENrecv for `node` with a driver callback (EmulNet.cpp:151-173): takes the node's
+ * messages off the EmulNet buffer in the reference's delivery order, counts them as received
+ * at `tick` (msgcount.log), and returns them with their payloads instead of queueing them.
+ * msgs == NULL: sizes only (*n messages, *n_payload entries), nothing taken.  A buffer too
+ * small for the sizes is GSP_ERR_CAPACITY with nothing taken. */
+int gsp_recv_detach(gsp_engine *e, int32_t tick, int32_t node, gsp_queued_msg *msgs, int32_t cap,
+                    gsp_entry *payload, int64_t payload_cap, int32_t *n, int64_t *n_payload);
+
+/* Queue::enqueue into `node`'s queue (Queue.h:22-26), processed by the node's next
+ * checkMessages / nodeLoop in queue order.  payload: m->payload_len entries, ids 1..N with
+ * port 0, each id once (the list the message carries); NULL: the payload is the sender's list
+ * of version m->send_batch, which the engine must still hold (GSP_ERR_ORDER otherwise). */
+int gsp_queue_push(gsp_engine *e, int32_t node, const gsp_queued_msg *m, const gsp_entry *payload);
+
+/* MP1Node::recvCallBack(env, data, size) called directly (MP1Node.cpp:219-260): `node`
+ * processes exactly this message now -- the merge, a JOINREP reply with its draw -- and its
+ * queue is left as it was.  payload as for gsp_queue_push. */
+int gsp_recv_callback(gsp_engine *e, int32_t tick, int32_t node, const gsp_queued_msg *m,
+                      const gsp_entry *payload, int32_t dropmsg);
 
 /* Every node's end-of-tick state appended to `path`, one line per node in id order:
  * "t id inited inGroup bFailed heartbeat |L| id:hb:ts ..." with the list in MemberListEntry

@@ -14,11 +14,18 @@
 // bFailed directly, Application.cpp:186/194); inited / inGroup / heartbeat are refreshed
 // after every batch; memberList is refreshed by MP1Node::syncMember() (one device read).
 //
-// Differences the batched engine imposes (documented in INTEGRATION.md):
-//   * recvCallBack(env, data, size) is executed inside checkMessages batches; a direct
-//     call with a raw buffer is rejected (returns false) because queued messages live in
-//     the engine, not in host memory;
-//   * ENrecv's enqueue callback and queue arguments are ignored for the same reason.
+// Receive paths (EmulNet.cpp:144-177, MP1Node.cpp:44-56, 200-260):
+//   * recvLoop (ENrecv with MP1Node::enqueueWrapper into the member's mp1q) is the batched
+//     path: the messages stay in the engine and checkMessages / nodeLoop drain them there;
+//   * ENrecv with any other callback or queue hands the callback each message as a heap
+//     MessageHdr (msgType, addr, vector_list = the sender's list at send time), in the
+//     reference's delivery order.  Whatever the callback puts into a member's mp1q is fed
+//     back to the engine, with the list it then holds, when that member next receives or
+//     processes (recvLoop / checkMessages / nodeLoop), and deleted as the reference's
+//     recvCallBack deletes each message it handles (MP1Node.cpp:258);
+//   * recvCallBack(env, data, size) called by the driver processes that one MessageHdr at
+//     once (the engine's gsp_recv_callback) and deletes it.
+// A MessageHdr list must name nodes of this emulation (ids 1..N, port 0), each at most once.
 #pragma once
 
 #include <cstdarg>
@@ -28,6 +35,7 @@
 #include <ctime>
 #include <queue>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "gossip/gossip.h"
@@ -156,6 +164,16 @@ struct Context {
     std::vector<int32_t> order;
     std::vector<int8_t> ops;
     std::vector<char> in_batch;
+    std::vector<Address> addrs;             // [i] = id i+1: MessageHdr::addr of handed messages
+    std::unordered_set<void *> issued;      // MessageHdrs handed to driver callbacks, unconsumed
+    bool snapshots = false;
+
+    // the engine keeps send-time lists once messages can be handled in separate batches
+    void enable_snapshots() {
+        if (snapshots) return;
+        if (gsp_payload_snapshots(engine, 1) != GSP_OK) die("gsp_payload_snapshots");
+        snapshots = true;
+    }
 
     static void die(const char *what) {
         std::fprintf(stderr, "gossip engine: %s failed: %s\n", what, gsp_last_error());
@@ -273,15 +291,14 @@ public:
         c.par = p;
         c.members.assign(size_t(p->EN_GPSZ), nullptr);
         c.in_batch.assign(size_t(p->EN_GPSZ), 0);
-    }
-    virtual ~EmulNet() {
-        auto &c = gsp_facade::ctx();
-        if (c.engine) {
-            c.flush();
-            gsp_destroy(c.engine);
-            c.engine = nullptr;
+        c.addrs.assign(size_t(p->EN_GPSZ), Address());
+        for (int i = 0; i < p->EN_GPSZ; ++i) {
+            const int id = i + 1;
+            std::memcpy(&c.addrs[size_t(i)].addr[0], &id, 4);
         }
+        c.snapshots = false;
     }
+    virtual ~EmulNet();
     void *ENinit(Address *myaddr, short /*port*/) {   // ids 1, 2, ... (EmulNet.cpp:72-77)
         const int id = nextid++;
         const short port = 0;
@@ -304,10 +321,8 @@ public:
         if (gsp_rand(c.engine, par->getcurrtime(), &v) != GSP_OK) c.die("gsp_rand");
         return v;
     }
-    int ENrecv(Address *myaddr, int (*)(void *, char *, int), struct timeval *, int, void *) {
-        gsp_facade::ctx().record(1, gsp_facade::node_of(myaddr), 0);
-        return 0;
-    }
+    int ENrecv(Address *myaddr, int (*enq)(void *, char *, int), struct timeval *t, int times,
+               void *queue);
     int ENcleanup() {   // writes msgcount.log for ticks [0, globaltime) (EmulNet.cpp:184-220)
         auto &c = gsp_facade::ctx();
         c.require_engine();
@@ -365,6 +380,7 @@ public:
 
     int recvLoop() {
         if (memberNode->bFailed) return false;
+        feed();
         return emulNet->ENrecv(&memberNode->addr, enqueueWrapper, nullptr, 1, &memberNode->mp1q);
     }
     static int enqueueWrapper(void *env, char *buff, int size) {
@@ -395,10 +411,14 @@ public:
     }
     void nodeLoop() {
         if (memberNode->bFailed) return;
+        feed();
         gsp_facade::ctx().record(2, node(), GSP_OP_LOOP);
     }
-    void checkMessages() { gsp_facade::ctx().record(2, node(), GSP_OP_CHECK); }
-    bool recvCallBack(void *, char *, int) { return false; }
+    void checkMessages() {
+        feed();
+        gsp_facade::ctx().record(2, node(), GSP_OP_CHECK);
+    }
+    bool recvCallBack(void *env, char *data, int size);
     void nodeLoopOps() { gsp_facade::ctx().record(2, node(), GSP_OP_OPS); }
     int isNullAddress(Address *a) {
         static const char zero[6] = {0};
@@ -432,6 +452,9 @@ public:
         return memberNode;
     }
 
+    // Hand what driver callbacks left in mp1q to the engine's queue of this node, in order.
+    void feed();
+
 private:
     int32_t node() const { return gsp_facade::node_of(&memberNode->addr); }
     Member *memberNode;
@@ -439,3 +462,123 @@ private:
     EmulNet *emulNet;
     Log *log;
 };
+
+namespace gsp_facade {
+
+// A MessageHdr as the engine's message: sender, type and the list it carries.
+inline bool to_msg(const MessageHdr *h, gsp_queued_msg &q, std::vector<gsp_entry> &list) {
+    if (h->msgType != JOINREQ && h->msgType != JOINREP && h->msgType != GOSSIP)
+        return false;   // no branch of recvCallBack handles it (MP1Node.cpp:221-257)
+    if (!h->addr) {
+        std::fprintf(stderr, "gossip engine: MessageHdr without addr\n");
+        std::exit(1);
+    }
+    q = gsp_queued_msg{};
+    q.src_id = h->addr->id();
+    q.type = int32_t(h->msgType);
+    q.send_batch = -1;
+    q.payload_len = int32_t(h->vector_list.size());
+    list.clear();
+    for (const MemberListEntry &e : h->vector_list)
+        list.push_back(gsp_entry{e.id, e.port, int64_t(e.heartbeat), int64_t(e.timestamp)});
+    return true;
+}
+
+inline const gsp_entry *list_ptr(const std::vector<gsp_entry> &list) {
+    static const gsp_entry none{};
+    return list.empty() ? &none : list.data();   // non-NULL: the list is the message's (empty)
+}
+
+inline void release(MessageHdr *h) {
+    ctx().issued.erase(h);
+    delete h;
+}
+
+}  // namespace gsp_facade
+
+inline EmulNet::~EmulNet() {
+    auto &c = gsp_facade::ctx();
+    if (c.engine) {
+        c.flush();
+        gsp_destroy(c.engine);
+        c.engine = nullptr;
+    }
+    for (void *h : c.issued) delete static_cast<MessageHdr *>(h);   // never handled
+    c.issued.clear();
+}
+
+inline int EmulNet::ENrecv(Address *myaddr, int (*enq)(void *, char *, int), struct timeval *,
+                           int, void *queue) {
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    const int32_t node = gsp_facade::node_of(myaddr);
+    if (node < 0 || size_t(node) >= c.members.size()) {
+        std::fprintf(stderr, "gossip engine: ENrecv for an unknown address\n");
+        std::exit(1);
+    }
+    Member *m = c.members[size_t(node)];
+    if (enq == &MP1Node::enqueueWrapper && m && queue == &m->mp1q) {
+        c.record(1, node, 0);   // batched: the messages stay in the engine's queue
+        return 0;
+    }
+    c.flush();
+    c.enable_snapshots();
+    const int t = par->getcurrtime();
+    int32_t n = 0;
+    int64_t np = 0;
+    if (gsp_recv_detach(c.engine, t, node, nullptr, 0, nullptr, 0, &n, &np) != GSP_OK)
+        c.die("gsp_recv_detach");
+    if (n == 0) return 0;
+    std::vector<gsp_queued_msg> msgs(static_cast<size_t>(n));
+    std::vector<gsp_entry> lists(size_t(np) + 1);
+    if (gsp_recv_detach(c.engine, t, node, msgs.data(), n, lists.data(), np, &n, &np) != GSP_OK)
+        c.die("gsp_recv_detach");
+    for (const gsp_queued_msg &q : msgs) {   // EmulNet.cpp:151-162: (*enq)(queue, tmp, sz)
+        MessageHdr *h = new MessageHdr();
+        h->msgType = MsgTypes(q.type);
+        h->addr = &c.addrs[size_t(q.src_id - 1)];
+        h->vector_list.reserve(size_t(q.payload_len));
+        for (int32_t i = 0; i < q.payload_len; ++i) {
+            const gsp_entry &e = lists[size_t(q.payload_off + i)];
+            h->vector_list.emplace_back(e.id, e.port, long(e.heartbeat), long(e.timestamp));
+        }
+        c.issued.insert(h);
+        enq(queue, reinterpret_cast<char *>(h), int(sizeof(MessageHdr)));
+    }
+    return 0;
+}
+
+inline void MP1Node::feed() {
+    auto &c = gsp_facade::ctx();
+    if (memberNode->mp1q.empty()) return;
+    // a batch already recorded for this node runs before these messages arrive
+    if (c.in_batch[size_t(node())]) c.flush();
+    gsp_queued_msg q;
+    std::vector<gsp_entry> list;
+    while (!memberNode->mp1q.empty()) {
+        MessageHdr *h = static_cast<MessageHdr *>(memberNode->mp1q.front().elt);
+        memberNode->mp1q.pop();
+        if (gsp_facade::to_msg(h, q, list) &&
+            gsp_queue_push(c.engine, node(), &q, gsp_facade::list_ptr(list)) != GSP_OK)
+            c.die("gsp_queue_push");
+        gsp_facade::release(h);
+    }
+}
+
+inline bool MP1Node::recvCallBack(void *, char *data, int) {
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    MessageHdr *h = reinterpret_cast<MessageHdr *>(data);
+    gsp_queued_msg q;
+    std::vector<gsp_entry> list;
+    if (gsp_facade::to_msg(h, q, list)) {
+        c.flush();
+        c.enable_snapshots();
+        if (gsp_recv_callback(c.engine, par->getcurrtime(), node(), &q, gsp_facade::list_ptr(list),
+                              par->dropmsg) != GSP_OK)
+            c.die("gsp_recv_callback");
+        c.refresh(node());
+    }
+    gsp_facade::release(h);
+    return true;
+}

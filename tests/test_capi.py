@@ -115,7 +115,8 @@ def test_struct_layouts_match_the_header():
     """Every public struct the ctypes stub mirrors has the C ABI's size."""
     L = _lib.lib()
     for name, cls in [("gsp_params", _lib.GspParams), ("gsp_member_view", _lib.GspMemberView),
-                      ("gsp_entry", _lib.GspEntry), ("gsp_exact_stats", _lib.GspExactStats),
+                      ("gsp_entry", _lib.GspEntry), ("gsp_queued_msg", _lib.GspQueuedMsg),
+                      ("gsp_exact_stats", _lib.GspExactStats),
                       ("gsp_fail_event", _lib.GspFailEvent), ("gsp_policy", _lib.GspPolicy),
                       ("gsp_scale_params", _lib.GspScaleParams),
                       ("gsp_scale_digest", _lib.GspScaleDigest),
@@ -123,7 +124,7 @@ def test_struct_layouts_match_the_header():
                       ("gsp_pview_params", _lib.GspPviewParams),
                       ("gsp_pview_digest", _lib.GspPviewDigest)]:
         assert L.gsp_struct_size(name.encode()) == ctypes.sizeof(cls), name
-    assert L.gsp_abi_version() == 4
+    assert L.gsp_abi_version() == 5
 
 
 def test_scale_params_from_reference_conf():
