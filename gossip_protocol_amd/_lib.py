@@ -134,6 +134,8 @@ SIGNATURES = {
                                         c_int32, c_int32]),
     "gsp_send": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                 P(c_int32)]),
+    "gsp_send_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
+                                     P(GspEntry), c_int32, P(c_int32)]),
     "gsp_rand": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
     "gsp_log": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, ctypes.c_char_p]),
     "gsp_set_failed": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32]),

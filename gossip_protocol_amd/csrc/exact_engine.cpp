@@ -790,7 +790,14 @@ int gsp_recv_callback(gsp_engine *e, int32_t tick, int32_t node, const gsp_queue
 
 int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
              int32_t dropmsg, int32_t *admitted) {
+    return gsp_send_list(e, tick, src_node, dst_id, type, dropmsg, nullptr, 0, admitted);
+}
+
+int gsp_send_list(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
+                  int32_t dropmsg, const gsp_entry *payload, int32_t n_payload, int32_t *admitted) {
     GSP_REQUIRE(e && admitted, GSP_ERR_INVALID, "gsp_send: NULL argument");
+    if (payload)
+        if (int rc = check_payload(e, payload, n_payload)) return rc;
     GSP_REQUIRE(src_node >= 0 && src_node < e->n, GSP_ERR_INVALID, "gsp_send: node %d", src_node);
     GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_send: tick %d", tick);
     GSP_REQUIRE(type == GSP_MSG_JOINREQ || type == GSP_MSG_JOINREP || type == GSP_MSG_GOSSIP,
@@ -810,9 +817,11 @@ int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int3
     if (int32_t(e->buf.size()) >= e->p.en_buff_size ||
         kMsgHdrBytes + kEnMsgBytes >= e->p.max_msg_size || (dropmsg && draw % 100 < thr))
         return GSP_OK;
-    // the payload of a GOSSIP is the sender's list as committed now
-    e->buf.push(NetMsg{src_id, dst_id, type, e->last_commit[src_node]});
-    e->admitted(src_id, e->last_commit[src_node]);
+    // the payload is the list handed in, or the sender's list as committed now
+    NetMsg m{src_id, dst_id, type, e->last_commit[src_node]};
+    if (payload) m.prow = e->pool_put(std::vector<gsp_entry>(payload, payload + n_payload));
+    else e->admitted(src_id, e->last_commit[src_node]);
+    e->buf.push(m);
     e->sent_host[size_t(src_id) * kMaxTicks + tick]++;
     e->stats.sends_admitted++;
     *admitted = kMsgHdrBytes;

@@ -169,6 +169,13 @@ int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out);
 /* The member list of `node` in list order (MemberListEntry vector order). */
 int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n);
 
+/* gsp_send with the message's own list (MessageHdr::vector_list of a message the driver
+ * built, MP1Node.cpp:355-359): `payload` holds n_payload entries (ids 1..N, port 0, each id
+ * once), which the receiver merges instead of the sender's committed list.  payload NULL is
+ * gsp_send. */
+int gsp_send_list(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int32_t type,
+                  int32_t dropmsg, const gsp_entry *payload, int32_t n_payload, int32_t *admitted);
+
 /* ---- Driver-side receive: EmulNet::ENrecv with the driver's own callback and direct
  * MP1Node::recvCallBack calls (MP1Node.cpp:46, 209, 219).  The reference hands the callback
  * each message as a MessageHdr whose vector_list is the sender's list at send time

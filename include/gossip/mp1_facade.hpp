@@ -346,15 +346,21 @@ typedef struct MessageHdr {
     std::vector<MemberListEntry> vector_list;
 } MessageHdr;
 
+// A message the driver built (MP1Node.cpp:355-359) carries its own vector_list.
 inline int EmulNet::ENsend(Address *myaddr, Address *toaddr, char *data, int /*size*/) {
     auto &c = gsp_facade::ctx();
     c.require_engine();
     c.flush();
     const MessageHdr *h = reinterpret_cast<const MessageHdr *>(data);
+    std::vector<gsp_entry> list;
+    for (const MemberListEntry &e : h->vector_list)
+        list.push_back(gsp_entry{e.id, e.port, int64_t(e.heartbeat), int64_t(e.timestamp)});
+    static const gsp_entry none{};
     int32_t admitted = 0;
-    if (gsp_send(c.engine, par->getcurrtime(), gsp_facade::node_of(myaddr), toaddr->id(),
-                 int32_t(h->msgType), par->dropmsg, &admitted) != GSP_OK)
-        c.die("gsp_send");
+    if (gsp_send_list(c.engine, par->getcurrtime(), gsp_facade::node_of(myaddr), toaddr->id(),
+                      int32_t(h->msgType), par->dropmsg, list.empty() ? &none : list.data(),
+                      int32_t(list.size()), &admitted) != GSP_OK)
+        c.die("gsp_send_list");
     return admitted;
 }
 

@@ -18,6 +18,11 @@
 //   filter    ENrecv into a driver list; drops GOSSIP from id 2 in ticks [150, 170),
 //             raises the heartbeat of id 5 in payloads from id 4 in ticks [200, 220),
 //             enqueues the rest into mp1q in reverse order, then nodeLoop
+//   inject    wrapper, plus a GOSSIP the driver builds itself each tick in [200, 210): from
+//             id 3 to id 5, its vector_list forged -- ids 1..9 at hb 100 + t, ts t (crashed
+//             nodes come back, the sender and the receiver appear in it) -- sent with
+//             EmulNet::ENsend (EmulNet.cpp:87-118)
+//   inject_direct   the same injection with the direct receive path
 // The last stdout line is a checksum over every message the callbacks saw.
 #include <cstdio>
 #include <cstdlib>
@@ -39,7 +44,7 @@ namespace {
 
 constexpr int kTicks = 700;
 
-enum Mode { kWrapper, kObserve, kDirect, kFilter };
+enum Mode { kWrapper, kObserve, kDirect, kFilter, kInject, kInjectDirect };
 
 struct Held {
     char *data;
@@ -115,7 +120,7 @@ struct Sim {
     void receive(int i) {
         Member *m = members[size_t(i)];
         g_node = i;
-        if (mode == kWrapper) {
+        if (mode == kWrapper || mode == kInject) {
             nodes[size_t(i)]->recvLoop();
         } else if (mode == kObserve) {
             net->ENrecv(&m->addr, observe_cb, NULL, 1, &m->mp1q);
@@ -130,7 +135,7 @@ struct Sim {
         std::vector<Held> held;
         held.swap(g_held[size_t(i)]);
         const int t = par->getcurrtime();
-        if (mode == kDirect) {
+        if (mode == kDirect || mode == kInjectDirect) {
             for (const Held &h : held) nd->recvCallBack(m, h.data, h.size);
             if (m->inGroup) nd->nodeLoopOps();
             return;
@@ -166,6 +171,15 @@ struct Sim {
                 if (i == 0 && t % 500 == 0) log->LOG(&members[size_t(i)]->addr, "@@time=%d", t);
             }
         }
+        if ((mode == kInject || mode == kInjectDirect) && t >= 200 && t < 210 && n > 4 &&
+            !members[2]->bFailed) {
+            // kept alive: the buffer's copy shares the list (EmulNet.cpp:99-104 copies the bytes)
+            MessageHdr *msg = new MessageHdr();
+            msg->msgType = GOSSIP;
+            msg->addr = &members[2]->addr;
+            for (int id = 1; id < 10; ++id) msg->vector_list.push_back(MemberListEntry(id, 0, 100 + t, t));
+            net->ENsend(&members[2]->addr, &members[4]->addr, (char *)msg, sizeof(MessageHdr));
+        }
         if (par->DROP_MSG && t == 50) par->dropmsg = 1;
         if (par->SINGLE_FAILURE && t == 100) {
             const int victim = GSP_DRAW() % n;
@@ -193,12 +207,13 @@ struct Sim {
 
 int main(int argc, char *argv[]) {
     if (argc != 3) {
-        std::fprintf(stderr, "usage: RecvDriver <conf> wrapper|observe|direct|filter\n");
+        std::fprintf(stderr, "usage: RecvDriver <conf> wrapper|observe|direct|filter|inject|inject_direct\n");
         return 2;
     }
     const std::string m = argv[2];
     const Mode mode = m == "observe" ? kObserve : m == "direct" ? kDirect
-                    : m == "filter" ? kFilter : kWrapper;
+                    : m == "filter" ? kFilter : m == "inject" ? kInject
+                    : m == "inject_direct" ? kInjectDirect : kWrapper;
 #ifdef GSP_DRIVER_REFERENCE
     const char *s = std::getenv("GSP_SEED");
     srand(s && *s ? unsigned(std::strtoul(s, NULL, 10)) : 1u);

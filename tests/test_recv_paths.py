@@ -4,7 +4,8 @@ MP1Node::recvCallBack calls (EmulNet.cpp:144-177, MP1Node.cpp:44-56, 200-260).
 tests/drivers/recv_driver.cpp runs the reference Application's schedule with the receive side
 driven four ways (wrapper = recvLoop; observe = own callback into mp1q; direct = own callback
 into a driver list, then recvCallBack per message; filter = drop / rewrite / reorder before
-checkMessages).  The one source is built against the reference's own classes
+checkMessages; inject = GOSSIPs the driver builds and sends with EmulNet::ENsend, with their
+own vector_list).  The one source is built against the reference's own classes
 (oracle/_ref/RecvDriver, compiled from /root/reference's sources) and against the facade over
 the GPU engine (gossip_protocol_amd/bin/RecvDriver); stdout (with a checksum of every payload
 the callbacks saw), dbg.log and msgcount.log must agree byte for byte.
@@ -58,7 +59,8 @@ def test_reference_driver_reproduces_the_golden_outputs(tmp_path, conf, mode):
         assert out[name] == golden("glibc", conf, 1, name), name
 
 
-CASES = [(c, m, 1) for c in CONFS for m in ("wrapper", "observe", "direct", "filter")] + \
+CASES = [(c, m, 1) for c in CONFS for m in ("wrapper", "observe", "direct", "filter", "inject",
+                                            "inject_direct")] + \
         [(c, m, 10) for c in CONFS for m in ("direct", "filter")]
 
 
@@ -69,7 +71,7 @@ def test_facade_receive_paths_match_the_reference(tmp_path, conf, mode, seed):
     _need(GPU_DRIVER)
     want = _run(REF_DRIVER, str(tmp_path / "ref"), conf, mode, seed)
     got = _run(GPU_DRIVER, str(tmp_path / "gpu"), conf, mode, seed)
-    if mode != "wrapper":
+    if mode not in ("wrapper", "inject"):                 # the callback modes see messages
         assert b"messages=0 " not in want["stdout"]
     for name in OUTPUTS:
         if got[name] != want[name]:
