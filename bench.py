@@ -38,6 +38,11 @@ FAIL_TICK = 10
 SEED = 0x5EED
 
 
+# xgmi_bytes_per_tick is accounted, not measured: the bytes the library hands to RCCL
+# (send/recv, all-gather, all-reduce) per tick, summed over ranks -- no link counter is read
+XGMI_SOURCE = "accounted: bytes passed to RCCL calls per tick (not a link counter)"
+
+
 def host_cpu():
     """CPU model and core counts of this host (the CPU baseline runs on one of them)."""
     model = None
@@ -252,7 +257,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
                    "parallelism": ("rows%d" % world if world > 1 else
                                    "rows%d-in-process" % group if group > 1 else "1gpu")},
         "merges_per_s": merges / el,
-        "xgmi_bytes_per_tick": xgmi, "exchange_csr_ms": xch_ms,
+        "xgmi_bytes_per_tick": xgmi, "xgmi_bytes_source": XGMI_SOURCE, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
                      "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
@@ -466,7 +471,7 @@ def summarize_full(r, nodes, steps, world):
                                    ("" if r["tiles"] == 1 else "-%dtiles" % r["tiles"])) if world > 1 else
                    "1gpu" if r["tiles"] == 1 else "1gpu-%dtiles" % r["tiles"]},
         "merges_per_s": r["merges"] / r["el"],
-        "xgmi_bytes_per_tick": r["xgmi_tick"],
+        "xgmi_bytes_per_tick": r["xgmi_tick"], "xgmi_bytes_source": XGMI_SOURCE,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
                      "kernel_ms_per_tick": r["kern_ms"], "launches_per_tick": r["tiles"],
