@@ -57,7 +57,7 @@ $(PKG)/bin/RecvDriver: tests/drivers/recv_driver.cpp $(LIB) include/gossip/mp1_f
 	g++ -O2 -std=c++17 -Wall -Iinclude -o $@ tests/drivers/recv_driver.cpp \
 	    -L$(PKG) -lgossip_amd -Wl,-rpath,'$$ORIGIN/..'
 
-oracle:
+oracle: lib
 	$(MAKE) -C oracle
 
 # kernel A/B variant: make lib-variant TAG=x VFLAGS=-DGSP_...  ->  $(PKG)/libgossip_amd.x.so

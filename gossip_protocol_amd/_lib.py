@@ -137,11 +137,16 @@ SIGNATURES = {
     "gsp_send_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                      P(GspEntry), c_int32, P(c_int32)]),
     "gsp_rand": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
+    "gsp_srand": (ctypes.c_int, [ctypes.c_void_p, c_uint64]),
     "gsp_log": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, ctypes.c_char_p]),
     "gsp_set_failed": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32]),
     "gsp_get_member": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspMemberView)]),
     "gsp_member_list": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(GspEntry), c_int32,
                                        P(c_int32)]),
+    "gsp_member_lists": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int32, P(GspEntry),
+                                        P(c_int32)]),
+    "gsp_add_member": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, P(GspEntry), c_int32,
+                                      P(c_int32)]),
     "gsp_payload_snapshots": (ctypes.c_int, [ctypes.c_void_p, c_int32]),
     "gsp_recv_detach": (ctypes.c_int, [ctypes.c_void_p, c_int32, c_int32, P(GspQueuedMsg), c_int32,
                                        P(GspEntry), c_int64, P(c_int32), P(c_int64)]),

@@ -279,6 +279,12 @@ int read_list(gsp_engine *e, int32_t node, std::vector<gsp_entry> &list) {
     return GSP_OK;
 }
 
+// Whether a message's merge reads its payload: GOSSIP always (MP1Node.cpp:244-256), JOINREP
+// only with the opt-in introducer list (the reference ignores it, :231-233), JOINREQ never.
+bool carries_payload(const gsp_engine *e, const NetMsg &m) {
+    return m.type == GSP_MSG_GOSSIP || (m.type == GSP_MSG_JOINREP && e->p.intro_list > 0);
+}
+
 // The payload of a queued message (the sender's list at send time, MP1Node.cpp:138/227/357):
 // *out = its pool list or the list kept from send time, or nullptr when it is the sender's
 // committed row (the sender has not committed since the send).
@@ -329,7 +335,19 @@ int make_msg(gsp_engine *e, int32_t node, const gsp_queued_msg *m, const gsp_ent
     if (payload) {
         if (int rc = check_payload(e, payload, m->payload_len)) return rc;
         out->prow = e->pool_put(std::vector<gsp_entry>(payload, payload + m->payload_len));
+        return GSP_OK;
     }
+    // NULL: the payload is the sender's list of version send_batch.  The engine must still
+    // hold it when the message carries one (GOSSIP, or JOINREP with an introducer list), and
+    // the message counts as one more carrier of that version until it is consumed -- a
+    // detached message already gave its count back (gsp_recv_detach -> consumed), so without
+    // this the version's refcount would drop twice and a list other in-flight messages still
+    // carry could be erased.
+    if (carries_payload(e, *out)) {
+        const std::vector<gsp_entry> *pl = nullptr;
+        if (int rc = payload_of(e, *out, &pl)) return rc;
+    }
+    e->admitted(out->src, out->send_batch);
     return GSP_OK;
 }
 
@@ -475,18 +493,6 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         hp_nlist.push_back(int32_t(list.size()));
         return int32_t(hp_nlist.size()) - 1;
     };
-    if (e->snapshots) {
-        // keep the lists in-flight messages carry before this batch commits newer ones
-        for (int32_t i = 0; i < n; ++i) {
-            const int32_t node = order[i];
-            if (node < 0 || node >= N) continue;   // rejected below
-            auto it = e->versions.find(version_key(node + 1, e->last_commit[node]));
-            if (it != e->versions.end() && it->second.refs > 0 && !it->second.kept) {
-                if (int rc = read_list(e, node, it->second.list)) return rc;
-                it->second.kept = true;
-            }
-        }
-    }
     for (int32_t i = 0; i < n; ++i) {
         const int32_t node = order[i];
         const int32_t op = ops[i];
@@ -504,7 +510,7 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
                         "gsp_tick_process: queue of node %d too long", node);
             for (const NetMsg &m : e->queue[node]) {
                 int32_t prow = -1;
-                if (m.type == GSP_MSG_GOSSIP || (m.type == GSP_MSG_JOINREP && e->p.intro_list > 0)) {
+                if (carries_payload(e, m)) {
                     // the payload is the sender's list at send time (MP1Node.cpp:357): its
                     // committed row while unchanged, else a kept or driver-handed list
                     const std::vector<gsp_entry> *pl = nullptr;
@@ -522,6 +528,20 @@ int gsp_tick_process(gsp_engine *e, int32_t tick, const int32_t *order, const in
         h_qoff[i + 1] = int32_t(h_qsrc.size());
         h_soff[i + 1] = h_soff[i] + njreq + 1 + N;
         h_repoff[i + 1] = h_repoff[i] + (op == GSP_OP_START ? 0 : njreq);
+    }
+    if (e->snapshots) {
+        // keep the lists messages still in flight carry before this batch commits newer ones.
+        // After this batch's own queues are consumed: the messages it merges read the committed
+        // rows before the commit, so only carriers outside the batch (the buffer, other nodes'
+        // queues, driver-held messages) need a kept copy -- one device read per such sender.
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t node = order[i];
+            auto it = e->versions.find(version_key(node + 1, e->last_commit[node]));
+            if (it != e->versions.end() && it->second.refs > 0 && !it->second.kept) {
+                if (int rc = read_list(e, node, it->second.list)) return rc;
+                it->second.kept = true;
+            }
+        }
     }
     const int32_t send_cap = h_soff[n];
     hipStream_t st = e->st;
@@ -722,9 +742,18 @@ int gsp_recv_detach(gsp_engine *e, int32_t tick, int32_t node, gsp_queued_msg *m
     int32_t cnt = 0;
     int64_t total = 0;
     int rc = GSP_OK;
+    static const std::vector<gsp_entry> kNoList;
+    // the list a driver callback sees: a JOINREP's send-time list, a driver-built list, an
+    // engine JOINREQ's empty list (nodeStart clears the list before introduceSelfToGroup sends
+    // it, MP1Node.cpp:95-150), or the sender's list of the message's version
+    auto list_of = [&](const NetMsg &m, const std::vector<gsp_entry> **pl) {
+        *pl = m.vrow >= 0 ? &e->pool[size_t(m.vrow)] : nullptr;
+        if (!*pl && m.prow < 0 && m.type == GSP_MSG_JOINREQ) *pl = &kNoList;
+        return *pl ? GSP_OK : payload_of(e, m, pl);
+    };
     e->buf.peek(id, [&](const NetMsg &m) {
-        const std::vector<gsp_entry> *pl = m.vrow >= 0 ? &e->pool[size_t(m.vrow)] : nullptr;
-        if (rc == GSP_OK && !pl) rc = payload_of(e, m, &pl);
+        const std::vector<gsp_entry> *pl = nullptr;
+        if (rc == GSP_OK) rc = list_of(m, &pl);
         cnt++;
         total += pl ? int64_t(pl->size()) : int64_t(e->nlist[size_t(m.src - 1)]);
     });
@@ -740,8 +769,8 @@ int gsp_recv_detach(gsp_engine *e, int32_t tick, int32_t node, gsp_queued_msg *m
     int64_t off = 0;
     e->buf.deliver(id, [&](const NetMsg &m) {                 // EmulNet.cpp:151-173
         e->recv_ctr[size_t(id) * kMaxTicks + tick]++;
-        const std::vector<gsp_entry> *pl = m.vrow >= 0 ? &e->pool[size_t(m.vrow)] : nullptr;
-        if (rc == GSP_OK && !pl) rc = payload_of(e, m, &pl);
+        const std::vector<gsp_entry> *pl = nullptr;
+        if (rc == GSP_OK) rc = list_of(m, &pl);
         if (rc == GSP_OK && !pl) {
             auto it = live.find(m.src);
             if (it == live.end()) {
@@ -840,6 +869,13 @@ int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value) {
     return GSP_OK;
 }
 
+int gsp_srand(gsp_engine *e, uint64_t seed) {
+    GSP_REQUIRE(e, GSP_ERR_INVALID, "gsp_srand: NULL engine");
+    e->seed = seed;
+    e->glibc.reseed_at(uint32_t(seed), e->draws);
+    return GSP_OK;
+}
+
 int gsp_log(gsp_engine *e, int32_t node, int32_t tick, const char *text) {
     GSP_REQUIRE(e && text, GSP_ERR_INVALID, "gsp_log: NULL argument");
     GSP_REQUIRE(node < e->n, GSP_ERR_INVALID, "gsp_log: node %d", node);
@@ -873,6 +909,100 @@ int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, in
     if (int rc = read_list(e, node, list)) return rc;
     *n = int32_t(list.size());
     for (int32_t k = 0; k < *n && k < cap; ++k) buf[k] = list[size_t(k)];
+    return GSP_OK;
+}
+
+int gsp_member_lists(gsp_engine *e, const int32_t *nodes, int32_t n, gsp_entry *buf,
+                     int32_t *lens) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(n >= 0 && (n == 0 || (nodes && buf && lens)), GSP_ERR_INVALID,
+                "gsp_member_lists: bad argument");
+    if (n == 0) return GSP_OK;
+    const int32_t N = e->n;
+    for (int32_t i = 0; i < n; ++i)
+        GSP_REQUIRE(nodes[i] >= 0 && nodes[i] < N, GSP_ERR_INVALID, "gsp_member_lists: node %d",
+                    nodes[i]);
+    // the whole committed table in one read per array (N <= 1024: at most 20 MB)
+    const size_t nn = size_t(N) * N;
+    std::vector<int64_t> key(nn);
+    std::vector<int32_t> hb(nn), ts(nn), rank(nn);
+    GSP_HIP(hipMemcpyAsync(key.data(), e->t_key.p, nn * 8, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(hb.data(), e->t_hb.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(ts.data(), e->t_ts.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipMemcpyAsync(rank.data(), e->t_rank.p, nn * 4, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    for (int32_t i = 0; i < n; ++i) {
+        const size_t row = size_t(nodes[i]) * N;
+        gsp_entry *out = buf + size_t(i) * N;
+        int32_t cnt = 0;
+        for (int32_t x = 0; x < N; ++x) {
+            if (key[row + x] < 0) continue;
+            GSP_REQUIRE(rank[row + x] >= 0 && rank[row + x] < N, GSP_ERR_INVALID, "corrupt rank");
+            out[rank[row + x]] = gsp_entry{x + 1, 0, hb[row + x], ts[row + x]};
+            cnt++;
+        }
+        lens[i] = cnt;
+    }
+    return GSP_OK;
+}
+
+int gsp_add_member(gsp_engine *e, int32_t tick, int32_t node, const gsp_entry *entry,
+                   int32_t mode, int32_t *added) {
+    if (int rc = check_engine(e)) return rc;
+    GSP_REQUIRE(entry && added && node >= 0 && node < e->n, GSP_ERR_INVALID,
+                "gsp_add_member: bad argument");
+    GSP_REQUIRE(mode == GSP_ADD_SENDER || mode == GSP_ADD_COPY, GSP_ERR_INVALID,
+                "gsp_add_member: mode %d", mode);
+    GSP_REQUIRE(tick >= 0 && tick < kMaxTicks, GSP_ERR_INVALID, "gsp_add_member: tick %d", tick);
+    const int32_t N = e->n, id = entry->id;
+    GSP_REQUIRE(id >= 1 && id <= N && entry->port == 0, GSP_ERR_INVALID,
+                "gsp_add_member: id %d port %d (ids 1..%d, port 0)", id, int(entry->port), N);
+    *added = 0;
+    const int32_t x = id - 1;
+    const size_t o = size_t(node) * N + size_t(x);
+    int64_t key = -1;
+    GSP_HIP(hipMemcpyAsync(&key, e->t_key.p + o, 8, hipMemcpyDeviceToHost, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    int32_t hb, ts;
+    if (mode == GSP_ADD_SENDER) {                               // MP1Node.cpp:265-280
+        if (key >= 0) return GSP_OK;                            // check_exist(id, port)
+        hb = 1;
+        ts = tick;
+    } else {                                                    // MP1Node.cpp:282-301
+        if (id == node + 1) return GSP_OK;                      // *addr == memberNode->addr
+        if (int64_t(tick) - entry->timestamp >= e->p.tremove) return GSP_OK;
+        GSP_REQUIRE(key < 0, GSP_ERR_INVALID,
+                    "gsp_add_member: id %d is listed already (the reference would list it twice)", id);
+        GSP_REQUIRE(entry->heartbeat >= INT32_MIN && entry->heartbeat <= INT32_MAX &&
+                    entry->timestamp >= INT32_MIN && entry->timestamp <= INT32_MAX,
+                    GSP_ERR_INVALID, "gsp_add_member: heartbeat/timestamp outside int32");
+        hb = int32_t(entry->heartbeat);
+        ts = int32_t(entry->timestamp);
+    }
+    // a new version of the list: keep the old one while messages in flight carry it
+    if (e->snapshots) {
+        auto it = e->versions.find(version_key(node + 1, e->last_commit[node]));
+        if (it != e->versions.end() && it->second.refs > 0 && !it->second.kept) {
+            if (int rc = read_list(e, node, it->second.list)) return rc;
+            it->second.kept = true;
+        }
+    }
+    // push_back: an insertion key above every key of earlier batches (make_key(batch, 0, 0),
+    // exact_kernels.hip), rank = the list length
+    const int64_t nkey = e->batch_seq << 40;
+    const int32_t rank = e->nlist[node];
+    const int32_t nl = rank + 1;
+    GSP_HIP(hipMemcpyAsync(e->t_key.p + o, &nkey, 8, hipMemcpyHostToDevice, e->st));
+    GSP_HIP(hipMemcpyAsync(e->t_hb.p + o, &hb, 4, hipMemcpyHostToDevice, e->st));
+    GSP_HIP(hipMemcpyAsync(e->t_ts.p + o, &ts, 4, hipMemcpyHostToDevice, e->st));
+    GSP_HIP(hipMemcpyAsync(e->t_rank.p + o, &rank, 4, hipMemcpyHostToDevice, e->st));
+    GSP_HIP(hipMemcpyAsync(e->t_state.p + 3 * size_t(N) + node, &nl, 4, hipMemcpyHostToDevice, e->st));
+    GSP_HIP(hipStreamSynchronize(e->st));
+    e->nlist[node] = nl;
+    e->last_commit[node] = e->batch_seq;
+    e->batch_seq++;
+    e->member_line(node, tick, x, "joined");                    // Log::logNodeAdd
+    *added = 1;
     return GSP_OK;
 }
 

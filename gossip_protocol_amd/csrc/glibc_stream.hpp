@@ -37,6 +37,12 @@ public:
         window_.clear();
     }
 
+    // srand(seed) issued after g draws: draw g is the first value of seed's stream
+    void reseed_at(uint32_t seed, int64_t g) {
+        reseed(seed);
+        base_ = g;
+    }
+
     // rand() value of draw index g (g = 0 is the first rand() after srand); g >= base().
     int32_t at(int64_t g) {
         fill_to(g + 1);

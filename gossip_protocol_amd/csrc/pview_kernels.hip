@@ -38,18 +38,6 @@
 #include <algorithm>
 #include <type_traits>
 
-#ifndef GSP_PV_K67_WAVES      // waves per SIMD the k = 6, 7 kernel is compiled for (A/B experiments)
-#define GSP_PV_K67_WAVES 8
-#endif
-#ifndef GSP_PV_K4_WAVES       // waves per SIMD of the in-place k = 4 / k = 5 kernels (14 / 12 rows
-#define GSP_PV_K4_WAVES 7     // per CU; 8 / 7 spill 24 / 20 B)
-#endif
-#ifndef GSP_PV_K5_WAVES
-#define GSP_PV_K5_WAVES 6
-#endif
-#ifndef GSP_PV_IP             // in-place rows (PvSharedIP), a bit mask: 1 k = 6, 7 as 128-lane in-place
-#define GSP_PV_IP 2           // rows (A/B +1.9 %), 2 k = 4, 5 in place (the default: -1.3 %), 4 k <= 3
-#endif                        // in place (±0)
 
 #include "join_kernels.hpp"
 #include "philox.hpp"
@@ -80,17 +68,6 @@ __device__ inline uint64_t pv_seed(uint32_t kind, uint32_t t, uint32_t r) {
     return z ^ (z >> 31);
 }
 __device__ inline uint32_t pv_hash(uint32_t s, uint32_t x) {
-#ifdef GSP_PV_EXP_NOHASH
-    return 0;
-#endif
-#ifdef GSP_PV_EXP_OLDHASH    // A/B only (round 3's per-event finaliser; not the oracle's digest)
-    uint32_t h = (x ^ s) * 0x9E3779B1u;
-    h ^= h >> 16;
-    h *= 0x85EBCA6Bu;
-    h ^= h >> 13;
-    uint32_t b = h * 0xC2B2AE35u;
-    return (b ^ (b >> 16) ^ h) >> 5;
-#endif
     return ((x ^ s) * 0x9E3779B1u) >> 5;
 }
 
@@ -983,7 +960,6 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
         }
     }
     pm.mark(0);
-#ifndef GSP_PV_EXP_NO_OWN_ONLY
     if constexpr ((kExt & ~kExtRot) == 0 && kQlo == 0) {   // (a row without messages evicts nothing)
         if (k == 0) {
             pv_own_only<NT>(a, sh, r, lr, ent0, ro);
@@ -993,7 +969,6 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
             return;
         }
     }
-#endif
     // one variant per key count (own view + k sender views)
 #define GSP_PV_VARIANT(K)                                                                        \
     else if (kQlo <= K && K <= kQhi && k == K)                                                  \
@@ -1400,11 +1375,7 @@ unsigned digest_blocks(int64_t records) {
 }
 
 void launch_send_and_digest(const PviewTickArgs &a, hipStream_t st) {
-#ifdef GSP_PV_EXP_SEND16
-    if (false)
-#else
     if (a.fanout <= 4)
-#endif
         hipLaunchKernelGGL(pview_send_kernel<4>, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
     else
         hipLaunchKernelGGL(pview_send_kernel<16>, dim3(unsigned((a.rows + 255) / 256)), dim3(256), 0, st, a);
@@ -1488,23 +1459,13 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         b.split_grid[3] = grid(0, 3);
         const int32_t cus = a.cus > 0 ? a.cus : 256;
         const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
-#if GSP_PV_IP & 1
-#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 6, 7, 5, true>), dim3(b.split_grid[0]), dim3(128), 0, st, b);
-#else
-#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, GSP_PV_K67_WAVES>), dim3(b.split_grid[0]), dim3(256), 0, st, b);
-#endif
-#if GSP_PV_IP & 2
-#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, GSP_PV_K5_WAVES, true>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
-#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, GSP_PV_K4_WAVES, true>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
-#else
-#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 5>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
-#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 6>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
-#endif
-#if GSP_PV_IP & 4
-#define GSP_PV_K03(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3, 8, true>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
-#else
+        // k = 6, 7: 256-lane rows in 20 KB, 8 waves per SIMD; k = 5 / k = 4: 128-lane rows merged in
+        // place (PvSharedIP, 11.3 / 9.8 KB) at 6 / 7 waves per SIMD (8 / 7 spill 24 / 20 B);
+        // k <= 3: 128-lane rows in 10 KB.  DESIGN.md 4b records the A/Bs behind each choice.
+#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, 8>), dim3(b.split_grid[0]), dim3(256), 0, st, b);
+#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 6, true>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
+#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 7, true>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
 #define GSP_PV_K03(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
-#endif
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
     do {                                                                                                  \
         if (b.split_grid[0]) GSP_PV_K67(E)                                                                \
@@ -1513,10 +1474,6 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         if (b.split_grid[3]) GSP_PV_K03(E)                                                                \
         if (!exact) hipLaunchKernelGGL((pview_tick_overflow_kernel<E>), dim3(gov), dim3(kPvBlock), 0, st, b); \
     } while (0)
-#ifdef GSP_PV_EXP_PLAIN_ONLY   // experiments: the plain protocol's kernels only (fast builds)
-        if (ext != 0) return hipErrorNotSupported;
-        GSP_PV_SPLIT_LAUNCH(0);
-#else
         switch (ext) {      // evict_order 1: the plain protocol's kernel, or the superset one
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
             case kExtEv: GSP_PV_SPLIT_LAUNCH(kExtEv); break;
@@ -1525,7 +1482,6 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
             case kExtRot: GSP_PV_SPLIT_LAUNCH(kExtRot); break;
             default: GSP_PV_SPLIT_LAUNCH(kExtRot | kExtPol | kExtEv); break;
         }
-#endif
 #undef GSP_PV_SPLIT_LAUNCH
 #undef GSP_PV_K67
 #undef GSP_PV_K5
@@ -1534,10 +1490,6 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         launch_send_and_digest(b, st);
         return hipGetLastError();
     }
-#ifdef GSP_PV_EXP_PLAIN_ONLY
-    if (ext != 0) return hipErrorNotSupported;
-    hipLaunchKernelGGL((pview_tick_kernel<0>), g, blk, 0, st, a);
-#else
     switch (ext) {
         case 0: hipLaunchKernelGGL((pview_tick_kernel<0>), g, blk, 0, st, a); break;
         case kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtEv>), g, blk, 0, st, a); break;
@@ -1545,7 +1497,6 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         case kExtPol | kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtPol | kExtEv>), g, blk, 0, st, a); break;
         default: hipLaunchKernelGGL((pview_tick_kernel<kExtRot | kExtPol | kExtEv>), g, blk, 0, st, a); break;
     }
-#endif
     launch_send_and_digest(a, st);
     return hipGetLastError();
 }

@@ -505,6 +505,28 @@ int collect_timing(gsp_scale *s) {
     return GSP_OK;
 }
 
+// scale_long_kernel's tile table: each tile's args at both tick parities (digest base at tick
+// 0, every tile reading its CSR owner's deferred-row list).  The long kernel patches only
+// tick, drop_pct, drop_prev and the digest offset per tick (scale_kernels.hip,
+// scale_long_kernel); every other field is read from here, so the table is rebuilt whenever
+// a field it copies can change after create (gsp_scale_set_cache_policy: nt_own / nt_src /
+// pipe).  An args field that changes per tick must join the kernel's patch list instead.
+int upload_long_tpl(gsp_scale *s) {
+    std::vector<gsp::ScaleTickArgs> tpl;
+    for (Shard &sh : s->local)
+        for (int32_t par = 0; par < 2; ++par) {
+            gsp::ScaleTickArgs x = s->args(sh, 2 + par);
+            x.dig = sh.dig.p;
+            x.long_list = s->long_list(sh, par);
+            tpl.push_back(x);
+        }
+    if (!s->long_tpl.p) GSP_HIP(s->long_tpl.alloc(tpl.size()));
+    GSP_HIP(hipStreamSynchronize(s->st));          // no queued launch still reads the old table
+    GSP_HIP(hipMemcpy(s->long_tpl.p, tpl.data(), tpl.size() * sizeof(gsp::ScaleTickArgs),
+                      hipMemcpyHostToDevice));
+    return GSP_OK;
+}
+
 int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t rank,
                 int32_t local_shards, const void *nccl_id, int32_t layout, gsp_scale **out) {
     GSP_REQUIRE(out, GSP_ERR_INVALID, "gsp_scale: out is NULL");
@@ -589,20 +611,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
         sh.rows = s->rowmode ? gsp::rowx_row0(sh.g + 1, p->n, shards) - sh.row0 : p->n;
         if (int rc = shard_alloc(s.get(), sh)) return rc;
     }
-    {   // scale_long_kernel's tile table: each tile's args at both tick parities, digest base
-        // at tick 0, every tile reading its CSR owner's deferred-row list
-        std::vector<gsp::ScaleTickArgs> tpl;
-        for (Shard &sh : s->local)
-            for (int32_t par = 0; par < 2; ++par) {
-                gsp::ScaleTickArgs x = s->args(sh, 2 + par);
-                x.dig = sh.dig.p;
-                x.long_list = s->long_list(sh, par);
-                tpl.push_back(x);
-            }
-        GSP_HIP(s->long_tpl.alloc(tpl.size()));
-        GSP_HIP(hipMemcpy(s->long_tpl.p, tpl.data(), tpl.size() * sizeof(gsp::ScaleTickArgs),
-                          hipMemcpyHostToDevice));
-    }
+    if (int rc = upload_long_tpl(s.get())) return rc;
     for (Shard &sh : s->local) GSP_HIP(gsp::launch_scale_init(s->args(sh, 0), s->sliced, s->st));
     if (s->sliced)
         if (int rc = resolve_sends(s.get(), 0)) return rc;
@@ -877,7 +886,7 @@ int gsp_scale_set_cache_policy(gsp_scale *s, int32_t policy) {
     GSP_REQUIRE(s && policy >= 0 && policy <= 7, GSP_ERR_INVALID,
                 "gsp_scale_set_cache_policy: policy %d", policy);
     s->policy = policy;
-    return GSP_OK;
+    return upload_long_tpl(s);
 }
 
 int gsp_scale_set_merge(gsp_scale *s, int32_t packed) {

@@ -330,13 +330,11 @@ __device__ __forceinline__ void scale_tick_row(const ScaleTickArgs &a, const int
             if (!kSlice && tid < F) a.out_dst[int64_t(lr) * F + tid] = -1;
             return;
         }
-#ifndef GSP_SCALE_EXP_NO_LONG          // A/B only: the tick kernel without the deferral
         if (!lng && k > kMaxSegment) {   // deferred to scale_long_kernel (one list per CSR)
             if (tid == 0 && a.long_list)
                 a.long_list[1 + atomicAdd(&a.long_list[0], 1)] = lr;
             return;
         }
-#endif
     }
     if constexpr (lng) {
         const int32_t o0 = a.off[lr];
@@ -751,9 +749,6 @@ __device__ __forceinline__ void scale_tick_row(const ScaleTickArgs &a, const int
         }
     }
     if (kSlice) return;
-#if GSP_SCALE_NOSEND   // measurement only: the merge without the send step (wrong protocol)
-    if (!kInit) { if (tid < F) a.out_dst[int64_t(lr) * F + tid] = -1; return; }
-#endif
 
     // send: wave 0 picks min(F, live) distinct members by Philox rank-select
     if (wave == 0) {
@@ -808,8 +803,9 @@ __global__ void __launch_bounds__(kScaleBlock) scale_tick_kernel(ScaleTickArgs a
 }
 
 // The rows the tick kernels deferred (k > kMaxSegment), after every tick-kernel launch of the
-// tick: tile g's args are its template of this tick's parity (made by the host at create) with
-// the tick's own fields; each tile's list is its CSR's (the tiles of an in-process group share
+// tick: tile g's args are its template of this tick's parity (made by the host, upload_long_tpl
+// in scale_engine.cpp) with the tick's own fields patched below -- tick, drop_pct, drop_prev,
+// the digest offset; a per-tick args field not in that list must be added there; each tile's list is its CSR's (the tiles of an in-process group share
 // one).  Launched once per tick; without a deferred row every workgroup reads the counts and
 // exits.  It also clears the lists of the next tick's parity.
 template <bool kSlice, bool kTfail, bool kSwim>
@@ -1084,9 +1080,6 @@ hipError_t launch_scale_tick(const ScaleTickArgs &a, bool slice, int merge, hipS
 hipError_t launch_scale_long(const ScaleTickArgs &a, const ScaleTickArgs *tpl, int32_t ntiles, bool slice,
                              hipStream_t st) {
     if (ntiles < 1) return hipErrorInvalidValue;
-#ifdef GSP_SCALE_EXP_NO_LONG
-    return hipSuccess;
-#endif
     const size_t lds = scale_lds_bytes(a.stride, slice, a.ev.buf != nullptr) + size_t(a.lds_pad);
     const dim3 grid(64), block(kScaleBlock);
     const int v = (slice ? 4 : 0) | (a.tfail > 0 ? 2 : 0) | (a.swim > 0 ? 1 : 0);

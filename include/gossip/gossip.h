@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 5
+#define GSP_ABI_VERSION 6
 
 typedef enum {
     GSP_OK = 0,
@@ -146,6 +146,11 @@ int gsp_send(gsp_engine *e, int32_t tick, int32_t src_node, int32_t dst_id, int3
  * Application.cpp:182/189).  In Philox mode the draw is Philox(seed; tick, 0, 0, 0). */
 int gsp_rand(gsp_engine *e, int32_t tick, int32_t *value);
 
+/* srand(seed) (Application.cpp:50/96): the next draw is the first of seed's stream (glibc
+ * mode: the TYPE_3 stream of srand(seed) restarts at that draw; Philox mode: seed becomes
+ * the replay key).  Draws already made are not affected. */
+int gsp_srand(gsp_engine *e, uint64_t seed);
+
 /* A line from the driver into dbg.log, ordered after all work submitted before it
  * (Log::LOG, Log.cpp:44).  node < 0 prints the empty address of the very first LOG. */
 int gsp_log(gsp_engine *e, int32_t node, int32_t tick, const char *text);
@@ -168,6 +173,25 @@ int gsp_set_failed(gsp_engine *e, int32_t node, int32_t failed);
 int gsp_get_member(gsp_engine *e, int32_t node, gsp_member_view *out);
 /* The member list of `node` in list order (MemberListEntry vector order). */
 int gsp_member_list(gsp_engine *e, int32_t node, gsp_entry *buf, int32_t cap, int32_t *n);
+/* The member lists of n nodes with one device read: list i (list order) at buf + i * N,
+ * N = max_nnb entries each, its length in lens[i]. */
+int gsp_member_lists(gsp_engine *e, const int32_t *nodes, int32_t n, gsp_entry *buf,
+                     int32_t *lens);
+
+/* MP1Node::addMember on `node`'s committed list at `tick` (MP1Node.cpp:265-301), a list
+ * change of its own (the list's send-time version changes as after a batch):
+ *  GSP_ADD_SENDER  addMember(MessageHdr *): entry->id absent -> appended as (id, 1, tick)
+ *                  with its "joined" dbg.log line; present -> nothing;
+ *  GSP_ADD_COPY    addMember(MemberListEntry *): the node itself -> nothing; else, when
+ *                  tick - entry->timestamp < TREMOVE, the entry is appended as given with its
+ *                  "joined" line.  The reference appends without looking the id up (its
+ *                  callers check_exist first); an id already listed is GSP_ERR_INVALID here,
+ *                  since a list holds each id once.
+ * entry: id 1..N, port 0 (heartbeat / timestamp within int32).  *added = 1 if appended. */
+#define GSP_ADD_SENDER 0
+#define GSP_ADD_COPY 1
+int gsp_add_member(gsp_engine *e, int32_t tick, int32_t node, const gsp_entry *entry,
+                   int32_t mode, int32_t *added);
 
 /* gsp_send with the message's own list (MessageHdr::vector_list of a message the driver
  * built, MP1Node.cpp:355-359): `payload` holds n_payload entries (ids 1..N, port 0, each id
@@ -193,9 +217,11 @@ typedef struct {
 } gsp_queued_msg;
 
 /* Keep each sender's send-time list while messages carry it and the sender commits a newer
- * one (off by default: the batched phases never need it).  Needed once messages can be
- * processed in separate batches (gsp_recv_callback), so the facade turns it on at the first
- * driver-callback receive. */
+ * one (off by default: a driver that runs each phase as one batch never needs it).  Needed
+ * once messages can be handled in separate batches (driver callbacks, gsp_recv_callback,
+ * gsp_add_member), so mp1_facade.hpp turns it on when its EmulNet is constructed: every
+ * message admitted from then on holds its list, whatever receive path the driver takes
+ * later. */
 int gsp_payload_snapshots(gsp_engine *e, int32_t on);
 
 /* EmulNet::ENrecv for `node` with a driver callback (EmulNet.cpp:151-173): takes the node's

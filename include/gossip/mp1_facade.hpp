@@ -11,8 +11,20 @@
 // EmulNet::ENsend/ENcleanup, or MP1Node::syncMember().
 //
 // Member is a host mirror.  bFailed and addr are driver-owned (Application::fail writes
-// bFailed directly, Application.cpp:186/194); inited / inGroup / heartbeat are refreshed
-// after every batch; memberList is refreshed by MP1Node::syncMember() (one device read).
+// bFailed directly, Application.cpp:186/194); inited / inGroup / heartbeat / nnb and
+// memberList are refreshed after every batch that ran the node (memberList with one device
+// read of the table per batch).  MP1Node::getMemberNode() first runs a batch the node is
+// recorded in, so a driver reading getMemberNode()->memberList sees what the reference's
+// list holds at that point.  The mirror is read-only: writes to memberList do not reach the
+// engine (MP1Node::addMember does).
+//
+// rand() / srand(): the reference's Application draws from libc rand() (fail(),
+// Application.cpp:182/189) on the stream its EmulNet draws from (EmulNet.cpp:89).  The
+// engine owns that stream, so the forwarding headers in include/gossip/ref/ (MP1Node.h,
+// EmulNet.h, ...) map rand() / srand() of the translation unit that includes them onto
+// gsp_mp1_rand() / gsp_mp1_srand() (include/gossip/ref/gsp_rand_interpose.h) -- srand(seed) seeds the engine's
+// stream (before the EmulNet exists: the seed it is created with), rand() runs the recorded
+// work and returns the stream's next draw.  Application.cpp then compiles unchanged.
 //
 // Receive paths (EmulNet.cpp:144-177, MP1Node.cpp:44-56, 200-260):
 //   * recvLoop (ENrecv with MP1Node::enqueueWrapper into the member's mp1q) is the batched
@@ -167,6 +179,10 @@ struct Context {
     std::vector<Address> addrs;             // [i] = id i+1: MessageHdr::addr of handed messages
     std::unordered_set<void *> issued;      // MessageHdrs handed to driver callbacks, unconsumed
     bool snapshots = false;
+    bool seeded = false;                    // srand() before the EmulNet: its seed
+    uint64_t seed = 0;
+    std::vector<gsp_entry> lists;           // gsp_member_lists scratch
+    std::vector<int32_t> lens;
 
     // the engine keeps send-time lists once messages can be handled in separate batches
     void enable_snapshots() {
@@ -194,7 +210,7 @@ struct Context {
             if (gsp_tick_process(engine, tick, order.data(), ops.data(), int32_t(order.size()),
                                  dropmsg) != GSP_OK)
                 die("gsp_tick_process");
-            for (int32_t node : order) refresh(node);
+            refresh_nodes(order);
         }
         for (int32_t node : order) in_batch[size_t(node)] = 0;
         order.clear();
@@ -211,6 +227,33 @@ struct Context {
         m->inGroup = v.in_group != 0;
         m->heartbeat = long(v.heartbeat);
         m->nnb = v.n_members;
+    }
+
+    // the scalar fields and the member lists of `nodes` (one device read for all lists)
+    void refresh_nodes(const std::vector<int32_t> &nodes) {
+        if (nodes.empty()) return;
+        const size_t N = members.size();
+        lists.resize(nodes.size() * N);
+        lens.resize(nodes.size());
+        if (gsp_member_lists(engine, nodes.data(), int32_t(nodes.size()), lists.data(),
+                             lens.data()) != GSP_OK)
+            die("gsp_member_lists");
+        for (size_t i = 0; i < nodes.size(); ++i) {
+            refresh(nodes[i]);
+            Member *m = members[size_t(nodes[i])];
+            if (!m) continue;
+            m->memberList.clear();
+            for (int32_t k = 0; k < lens[i]; ++k) {
+                const gsp_entry &e = lists[i * N + size_t(k)];
+                m->memberList.emplace_back(e.id, e.port, long(e.heartbeat), long(e.timestamp));
+            }
+        }
+    }
+    void refresh_node(int32_t node) { refresh_nodes(std::vector<int32_t>{node}); }
+
+    // a node whose calls are recorded but not yet run: run them (its mirror is then current)
+    void settle(int32_t node) {
+        if (node >= 0 && size_t(node) < in_batch.size() && in_batch[size_t(node)]) flush();
     }
 
     void record(int k, int32_t node, int8_t op) {
@@ -280,8 +323,12 @@ public:
     // counter-based replay stream; GSP_DEVICE selects the HIP device.
     explicit EmulNet(Params *p) : par(p) {
         auto &c = gsp_facade::ctx();
+        // the seed: srand()'s when the driver seeded before constructing the EmulNet
+        // (Application.cpp:50, with the forwarding headers' rand interposition), else
+        // GSP_SEED, else time(NULL) as srand(time(NULL))
         const char *s = std::getenv("GSP_SEED");
-        const uint64_t seed = s && *s ? std::strtoull(s, nullptr, 10) : uint64_t(std::time(nullptr));
+        const uint64_t seed = c.seeded ? c.seed
+                              : s && *s ? std::strtoull(s, nullptr, 10) : uint64_t(std::time(nullptr));
         const char *m = std::getenv("GSP_RNG");
         const gsp_rng_mode rng = (m && std::strcmp(m, "philox") == 0) ? GSP_RNG_PHILOX : GSP_RNG_GLIBC;
         const char *d = std::getenv("GSP_DEVICE");
@@ -296,7 +343,10 @@ public:
             const int id = i + 1;
             std::memcpy(&c.addrs[size_t(i)].addr[0], &id, 4);
         }
+        // send-time lists are kept from the first message on, so a driver may switch from
+        // recvLoop to its own ENrecv callback / recvCallBack / addMember at any tick
         c.snapshots = false;
+        c.enable_snapshots();
     }
     virtual ~EmulNet();
     void *ENinit(Address *myaddr, short /*port*/) {   // ids 1, 2, ... (EmulNet.cpp:72-77)
@@ -382,7 +432,10 @@ public:
         if (node >= 0 && size_t(node) < c.members.size()) c.members[size_t(node)] = member;
     }
     virtual ~MP1Node() {}
-    Member *getMemberNode() { return memberNode; }
+    Member *getMemberNode() {
+        gsp_facade::ctx().settle(node());
+        return memberNode;
+    }
 
     int recvLoop() {
         if (memberNode->bFailed) return false;
@@ -426,6 +479,17 @@ public:
     }
     bool recvCallBack(void *env, char *data, int size);
     void nodeLoopOps() { gsp_facade::ctx().record(2, node(), GSP_OP_OPS); }
+    // MP1Node.h:77-80.  addMember changes the engine's list (gsp_add_member); check_exist
+    // returns the entry of the (current) mirror, or nullptr.
+    void addMember(MessageHdr *messageHdr);
+    void addMember(MemberListEntry *m);
+    MemberListEntry *check_exist(int id, short port) {
+        gsp_facade::ctx().settle(node());
+        for (MemberListEntry &e : memberNode->memberList)
+            if (e.id == id && e.port == port) return &e;
+        return nullptr;
+    }
+    MemberListEntry *check_exist(Address *addr) { return check_exist(addr->id(), addr->port()); }
     int isNullAddress(Address *a) {
         static const char zero[6] = {0};
         return std::memcmp(a->addr, zero, 6) == 0 ? 1 : 0;
@@ -441,20 +505,12 @@ public:
         std::printf("%d.%d.%d.%d:%d \n", a->addr[0], a->addr[1], a->addr[2], a->addr[3],
                     int(a->port()));
     }
-    // Flush pending work and copy this node's member list from the device into the mirror.
+    // Run all recorded work and re-read this node's mirror from the device (kept from ABI 5;
+    // the mirror is current after every batch now).
     Member *syncMember() {
         auto &c = gsp_facade::ctx();
         c.flush();
-        c.refresh(node());
-        std::vector<gsp_entry> buf(size_t(par->EN_GPSZ) + 1);
-        int32_t n = 0;
-        if (gsp_member_list(c.engine, node(), buf.data(), int32_t(buf.size()), &n) != GSP_OK)
-            c.die("gsp_member_list");
-        memberNode->memberList.clear();
-        for (int32_t i = 0; i < n; ++i)
-            memberNode->memberList.emplace_back(buf[size_t(i)].id, buf[size_t(i)].port,
-                                                long(buf[size_t(i)].heartbeat),
-                                                long(buf[size_t(i)].timestamp));
+        c.refresh_node(node());
         return memberNode;
     }
 
@@ -583,8 +639,51 @@ inline bool MP1Node::recvCallBack(void *, char *data, int) {
         if (gsp_recv_callback(c.engine, par->getcurrtime(), node(), &q, gsp_facade::list_ptr(list),
                               par->dropmsg) != GSP_OK)
             c.die("gsp_recv_callback");
-        c.refresh(node());
+        c.refresh_node(node());
     }
     gsp_facade::release(h);
     return true;
+}
+
+inline void MP1Node::addMember(MessageHdr *messageHdr) {   // MP1Node.cpp:265-280
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    c.flush();
+    const gsp_entry e{messageHdr->addr->id(), messageHdr->addr->port(), 1, par->getcurrtime()};
+    int32_t added = 0;
+    if (gsp_add_member(c.engine, par->getcurrtime(), node(), &e, GSP_ADD_SENDER, &added) != GSP_OK)
+        c.die("gsp_add_member");
+    if (added) c.refresh_node(node());
+}
+
+inline void MP1Node::addMember(MemberListEntry *m) {        // MP1Node.cpp:282-301
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    c.flush();
+    const gsp_entry e{m->id, m->port, int64_t(m->heartbeat), int64_t(m->timestamp)};
+    int32_t added = 0;
+    if (gsp_add_member(c.engine, par->getcurrtime(), node(), &e, GSP_ADD_COPY, &added) != GSP_OK)
+        c.die("gsp_add_member");
+    if (added) c.refresh_node(node());
+}
+
+// rand() / srand() of a driver that shares its stream with EmulNet (header comment).
+inline void gsp_mp1_srand(unsigned int seed) {
+    auto &c = gsp_facade::ctx();
+    if (!c.engine) {                  // before the EmulNet: the seed it is created with
+        c.seeded = true;
+        c.seed = seed;
+        return;
+    }
+    c.flush();                        // recorded sends draw from the stream they were made on
+    if (gsp_srand(c.engine, seed) != GSP_OK) c.die("gsp_srand");
+}
+
+inline int gsp_mp1_rand() {
+    auto &c = gsp_facade::ctx();
+    c.require_engine();
+    c.flush();
+    int32_t v = 0;
+    if (gsp_rand(c.engine, c.par->getcurrtime(), &v) != GSP_OK) c.die("gsp_rand");
+    return v;
 }

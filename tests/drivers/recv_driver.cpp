@@ -23,7 +23,13 @@
 //             nodes come back, the sender and the receiver appear in it) -- sent with
 //             EmulNet::ENsend (EmulNet.cpp:87-118)
 //   inject_direct   the same injection with the direct receive path
-// The last stdout line is a checksum over every message the callbacks saw.
+//   switch    wrapper up to tick 119, direct from tick 120 on (a driver that changes receive
+//             path while messages sent under the batched path are still in flight)
+//   members   wrapper; after every tick each node's getMemberNode()->memberList goes into the
+//             checksum (the mirror is current), and in ticks [250, 260) node index 1 calls
+//             check_exist / addMember (MP1Node.cpp:265-326) on ids 9 and 8
+// The last stdout line is a checksum over every message the callbacks saw (and in `members`
+// mode every member list read).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,7 +50,7 @@ namespace {
 
 constexpr int kTicks = 700;
 
-enum Mode { kWrapper, kObserve, kDirect, kFilter, kInject, kInjectDirect };
+enum Mode { kWrapper, kObserve, kDirect, kFilter, kInject, kInjectDirect, kSwitch, kMembers };
 
 struct Held {
     char *data;
@@ -117,9 +123,16 @@ struct Sim {
 
     int start(int i) const { return int(par->STEP_RATE * i); }
 
+    // the receive path of this tick (switch: batched first, then the direct path)
+    Mode path() const {
+        if (mode == kSwitch) return par->getcurrtime() < 120 ? kWrapper : kDirect;
+        return mode == kMembers ? kWrapper : mode;
+    }
+
     void receive(int i) {
         Member *m = members[size_t(i)];
         g_node = i;
+        const Mode mode = path();
         if (mode == kWrapper || mode == kInject) {
             nodes[size_t(i)]->recvLoop();
         } else if (mode == kObserve) {
@@ -135,6 +148,7 @@ struct Sim {
         std::vector<Held> held;
         held.swap(g_held[size_t(i)]);
         const int t = par->getcurrtime();
+        const Mode mode = path();
         if (mode == kDirect || mode == kInjectDirect) {
             for (const Held &h : held) nd->recvCallBack(m, h.data, h.size);
             if (m->inGroup) nd->nodeLoopOps();
@@ -171,6 +185,7 @@ struct Sim {
                 if (i == 0 && t % 500 == 0) log->LOG(&members[size_t(i)]->addr, "@@time=%d", t);
             }
         }
+        if (mode == kMembers) members_step(t);
         if ((mode == kInject || mode == kInjectDirect) && t >= 200 && t < 210 && n > 4 &&
             !members[2]->bFailed) {
             // kept alive: the buffer's copy shares the list (EmulNet.cpp:99-104 copies the bytes)
@@ -195,6 +210,40 @@ struct Sim {
         if (par->DROP_MSG && t == 300) par->dropmsg = 0;
     }
 
+    // mode members: the public member-list surface of MP1Node (MP1Node.h:77-80, Member.h:112)
+    void members_step(int t) {
+        const int n = par->EN_GPSZ;
+        if (t >= 250 && t < 260 && n > 8 && !members[1]->bFailed && members[1]->inGroup) {
+            MP1Node *nd = nodes[1];
+            MemberListEntry *e9 = nd->check_exist(9, 0);
+            std::cout << "t " << t << " check_exist(9) " << (e9 ? e9->heartbeat : -1) << std::endl;
+            if (!e9) {                                   // a fresh copy, as recvCallBack adds one
+                MemberListEntry fresh(9, 0, 77 + t, t - 3);
+                nd->addMember(&fresh);
+            }
+            MessageHdr hdr;                              // addMember(hdr): id 8 at (1, t) if absent
+            hdr.msgType = GOSSIP;
+            hdr.addr = &members[7]->addr;
+            nd->addMember(&hdr);
+            MemberListEntry *e8 = nd->check_exist(&members[7]->addr);
+            std::cout << "t " << t << " check_exist(8) " << (e8 ? e8->heartbeat : -1) << " "
+                      << (e8 ? e8->timestamp : -1) << std::endl;
+        }
+        for (int i = 0; i < n; ++i) {                    // every list, read through the mirror
+            const std::vector<MemberListEntry> &l = nodes[size_t(i)]->getMemberNode()->memberList;
+            unsigned long long s = 1469598103934665603ull;
+            auto mix = [&](long long v) { s = (s ^ (unsigned long long)v) * 1099511628211ull; };
+            mix(t);
+            mix(i);
+            for (size_t k = 0; k < l.size(); ++k) {
+                mix(l[k].id);
+                mix(l[k].heartbeat);
+                mix(l[k].timestamp);
+            }
+            g_sum += s;
+        }
+    }
+
     void run() {
         for (par->globaltime = 0; par->globaltime < kTicks; ++par->globaltime) tick();
         net->ENcleanup();
@@ -207,13 +256,15 @@ struct Sim {
 
 int main(int argc, char *argv[]) {
     if (argc != 3) {
-        std::fprintf(stderr, "usage: RecvDriver <conf> wrapper|observe|direct|filter|inject|inject_direct\n");
+        std::fprintf(stderr, "usage: RecvDriver <conf> wrapper|observe|direct|filter|inject|inject_direct|"
+                             "switch|members\n");
         return 2;
     }
     const std::string m = argv[2];
     const Mode mode = m == "observe" ? kObserve : m == "direct" ? kDirect
                     : m == "filter" ? kFilter : m == "inject" ? kInject
-                    : m == "inject_direct" ? kInjectDirect : kWrapper;
+                    : m == "inject_direct" ? kInjectDirect : m == "switch" ? kSwitch
+                    : m == "members" ? kMembers : kWrapper;
 #ifdef GSP_DRIVER_REFERENCE
     const char *s = std::getenv("GSP_SEED");
     srand(s && *s ? unsigned(std::strtoul(s, NULL, 10)) : 1u);

@@ -1,4 +1,16 @@
-"""The drop-in `Application` binary (gossip_protocol_amd/bin/Application) on the GPU.
+"""The drop-in `Application` binaries on the GPU.
+
+oracle/_ref/Application_facade is the reference's OWN Application.cpp (/root/reference,
+unmodified), compiled against the forwarding headers include/gossip/ref/ and linked with
+libgossip_amd.so (oracle/Makefile; a test binary, never the product).  Its time() is pinned by
+GSP_SEED exactly as oracle/_ref/Application's is (oracle/ref_time_pin.c), so its two
+srand(time(NULL)) calls (Application.cpp:50, 96) seed the engine with the golden run's seed:
+* stdout, dbg.log and msgcount.log equal the reference's byte for byte, 3 testcases x 5 seeds x
+  {glibc, philox} (GSP_RNG=philox: the engine's Philox stream, as oracle/_ref/Application_replay);
+* with the wall-clock seed, Grader.sh's checks (tests/grader.py) give 90/90.
+
+gossip_protocol_amd/bin/Application is the build's own Application-shaped driver
+(gossip_protocol_amd/app/app_main.cpp) on the same facade.
 
 It is built only from the MP1Node / EmulNet / Params / Log facade (include/gossip/
 mp1_facade.hpp) and is run exactly the way Grader.sh runs the reference
@@ -13,22 +25,65 @@ import subprocess
 
 import pytest
 
-from tests.oracle_binding import CONFS, conf_path, golden
+from tests.oracle_binding import CONFS, MODES, SEEDS, conf_path, golden
 from tests import grader
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 APP = os.path.join(ROOT, "gossip_protocol_amd", "bin", "Application")
+REF_APP = os.path.join(ROOT, "oracle", "_ref", "Application_facade")
 
 
-def _run(tmp, conf, env_extra):
+def _run(tmp, conf, env_extra, app=APP):
     os.makedirs(os.path.join(tmp, "testcases"), exist_ok=True)
     shutil.copy(conf_path(conf), os.path.join(tmp, "testcases"))
     env = dict(os.environ, **env_extra)
-    r = subprocess.run([APP, "testcases/%s.conf" % conf], cwd=tmp, env=env, capture_output=True,
+    r = subprocess.run([app, "testcases/%s.conf" % conf], cwd=tmp, env=env, capture_output=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr.decode()
     return r.stdout
+
+
+def _need_ref_app():
+    if not os.path.exists(REF_APP):
+        pytest.fail("oracle/_ref/Application_facade is missing: build it here with `make -C oracle` "
+                    "(it needs /root/reference and gossip_protocol_amd/libgossip_amd.so)")
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("conf", CONFS)
+def test_reference_application_on_facade(tmp_path, conf, seed, mode):
+    """The reference's unmodified Application.cpp on the engine = the reference, byte for byte."""
+    _need_ref_app()
+    env = {"GSP_SEED": str(seed)}
+    if mode == "philox":
+        env["GSP_RNG"] = "philox"
+    else:
+        env["GSP_RNG"] = "glibc"
+    out = _run(str(tmp_path), conf, env, app=REF_APP)
+    assert out == golden(mode, conf, seed, "stdout.txt")
+    for name in ["dbg.log", "msgcount.log"]:
+        with open(os.path.join(str(tmp_path), name), "rb") as f:
+            assert f.read() == golden(mode, conf, seed, name), name
+    assert os.path.exists(os.path.join(str(tmp_path), "stats.log"))
+
+
+def test_reference_application_on_facade_grader_90(tmp_path):
+    """Grader.sh's scenarios with the wall-clock seed (no GSP_SEED: time() is libc's)."""
+    _need_ref_app()
+    total = 0
+    env = {k: v for k, v in os.environ.items() if k not in ("GSP_SEED", "GSP_RNG")}
+    for conf in CONFS:
+        d = os.path.join(str(tmp_path), conf)
+        os.makedirs(os.path.join(d, "testcases"))
+        shutil.copy(conf_path(conf), os.path.join(d, "testcases"))
+        r = subprocess.run([REF_APP, "testcases/%s.conf" % conf], cwd=d, env=env,
+                           capture_output=True, timeout=120)
+        assert r.returncode == 0, r.stderr.decode()
+        with open(os.path.join(d, "dbg.log"), "rb") as f:
+            total += grader.score(f.read(), conf)
+    assert total == 90
 
 
 @pytest.mark.parametrize("mode", ["glibc", "philox"])

@@ -1,6 +1,8 @@
 """The drop-in facade (include/gossip/mp1_facade.hpp) as a C++ maintainer compiles it: the header
 alone, the Grader-compatible Application driver and the receive-path test driver all compile
-warning-free under -Wall -Wextra -Werror (CPU only: syntax and types, no GPU, no link)."""
+warning-free under -Wall -Wextra -Werror; and the reference's own Application.cpp, unchanged,
+compiles against the forwarding headers of include/gossip/ref/ with rand() / srand() bound to
+the engine (CPU only: syntax, types and symbols, no GPU)."""
 import os
 import shutil
 import subprocess
@@ -28,3 +30,24 @@ def test_facade_compiles_warning_free(tmp_path, what):
                         "-I" + os.path.join(ROOT, "include"), src], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+REF = "/root/reference"
+
+
+def test_reference_application_compiles_unchanged(tmp_path):
+    """/root/reference/Application.cpp, compiled in place with the forwarding headers first on
+    the include path (-I-: its own directory is not searched first for "MP1Node.h" & co), uses
+    the facade's classes and the engine's draw stream: the object references gsp_* entry points
+    and no libc rand() / srand()."""
+    if shutil.which("g++") is None or not os.path.exists(os.path.join(REF, "Application.cpp")):
+        pytest.skip("no g++ or no reference tree")
+    obj = str(tmp_path / "app.o")
+    r = subprocess.run(["g++", "-std=c++11", "-w", "-c", "-I" + os.path.join(ROOT, "include", "gossip", "ref"),
+                        "-I-", "-I" + REF, "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(REF, "Application.cpp"), "-o", obj],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    syms = subprocess.run(["nm", "-u", obj], capture_output=True, text=True).stdout.split()
+    assert "gsp_rand" in syms and "gsp_srand" in syms and "gsp_tick_process" in syms
+    assert "rand" not in syms and "srand" not in syms

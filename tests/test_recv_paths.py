@@ -47,7 +47,7 @@ def _need(path):
         pytest.skip("%s not built (make app; make -C oracle with /root/reference present)" % path)
 
 
-@pytest.mark.parametrize("mode", ["wrapper", "observe", "direct"])
+@pytest.mark.parametrize("mode", ["wrapper", "observe", "direct", "switch"])
 @pytest.mark.parametrize("conf", CONFS)
 def test_reference_driver_reproduces_the_golden_outputs(tmp_path, conf, mode):
     """The driver is a faithful Application: on the reference's own classes, the receive
@@ -60,8 +60,8 @@ def test_reference_driver_reproduces_the_golden_outputs(tmp_path, conf, mode):
 
 
 CASES = [(c, m, 1) for c in CONFS for m in ("wrapper", "observe", "direct", "filter", "inject",
-                                            "inject_direct")] + \
-        [(c, m, 10) for c in CONFS for m in ("direct", "filter")]
+                                            "inject_direct", "switch", "members")] + \
+        [(c, m, 10) for c in CONFS for m in ("direct", "filter", "switch", "members")]
 
 
 @pytest.mark.gpu
