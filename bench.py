@@ -248,6 +248,8 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         return ev
     achieved = bytes_per_tick / (kern_ms * 1e-3) / 1e9
     peak = PEAK_HBM_GBS * world
+    window = [warmup + 1, warmup + steps]
+    traffic, traffic_note = _pview_traffic(nodes, world, window)
     out = {
         "metric": "gossip node-rounds/sec (partial view)", "value": rounds / el,
         "unit": "node-rounds/s", "ms_per_step": el * 1e3 / steps, "scaling": "strong",
@@ -259,45 +261,76 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "merges_per_s": merges / el,
         "xgmi_bytes_per_tick": xgmi, "xgmi_bytes_source": XGMI_SOURCE, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": _pview_traffic(nodes, world),
+                     "frac": achieved / peak, "traffic": traffic,
                      "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
-                     "valu": _pview_valu(nodes, world, kern_ms),
+                     "valu": _pview_valu(nodes, world, kern_ms, window),
+                     "window_ticks": window,
                      "kernel_ms_per_tick": kern_ms, "algorithmic_bytes_per_tick": bytes_per_tick},
     }
+    if traffic_note:
+        out["roofline"]["traffic_note"] = traffic_note
     if world == 1 and cpu_baseline_on:
         out["cpu_baseline"] = pview_cpu_baseline()
     return out
 
 
-def _pview_traffic(nodes, world):
-    """HBM bytes per tick-kernel launch from the committed PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE, scripts/pmc_traffic.py --pview) for the one-GPU config-5 run, else None."""
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic_pview.json")
-    if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
-        return None
+def _pmc(name, window):
+    """A committed PMC summary (profiles/<name>) if it was taken over exactly this run's tick
+    window, else (None, the window it covers).  Counter-derived fields are printed only for the
+    window they were measured on: the counts of ticks 6-25 say nothing
+    about, and must not be divided by the kernel time of, any other window."""
+    prof = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(prof):
+        return None, None
     try:
-        return json.load(open(prof)).get("bytes_per_launch")
+        d = json.load(open(prof))
     except Exception:
-        return None
+        return None, None
+    w = d.get("window_ticks")
+    if w is None or list(w) != list(window):
+        return None, w
+    return d, w
 
 
-def _pview_valu(nodes, world, kern_ms):
-    """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per launch from the
-    committed PMC pass (profiles/pmc_sq_pview.json, scripts/gpu_run.sh) over the live mean
-    kernel time: wave64 VALU instructions issued per SIMD cycle (1,024 SIMDs at 2.4 GHz), and
-    that rate against the SIMD's issue ceiling -- one wave64 VALU instruction per 2 cycles
-    with two or more waves resident (MI355X_MICROARCH.md, "Wave scheduling" and the
-    v_fma_f32 row of the constants table; 4 cycles is one wave alone); config 5, one GPU."""
-    prof = os.path.join(ROOT, "profiles", "pmc_sq_pview.json")
-    if nodes != PV_NODES or world != 1 or not os.path.exists(prof):
+def _window_note(name, have, window):
+    return ("null: profiles/%s covers ticks %d-%d, this run timed ticks %d-%d" %
+            (name, have[0], have[1], window[0], window[1])) if have else None
+
+
+def _pview_traffic(nodes, world, window):
+    """HBM bytes per tick from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
+    scripts/pmc_traffic.py --pview) for the one-GPU config-5 run over the same tick window,
+    else (None, note)."""
+    if nodes != PV_NODES or world != 1:
+        return None, None
+    d, w = _pmc("pmc_traffic_pview.json", window)
+    if d is None:
+        return None, _window_note("pmc_traffic_pview.json", w, window)
+    return d.get("bytes_per_launch"), None
+
+
+def _pview_valu(nodes, world, kern_ms, window):
+    """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per tick from the committed
+    PMC pass over the same tick window (profiles/pmc_sq_pview.json) over the live mean kernel
+    time: wave64 VALU instructions issued per SIMD cycle (1,024 SIMDs at 2.4 GHz), and that rate
+    against the SIMD's issue ceiling -- one wave64 VALU instruction per 2 cycles with two or more
+    waves resident (MI355X_MICROARCH.md, "Wave scheduling" and the v_fma_f32 row of the
+    constants table; 4 cycles is one wave alone); config 5, one GPU."""
+    if nodes != PV_NODES or world != 1:
         return None
+    d, w = _pmc("pmc_sq_pview.json", window)
+    if d is None:
+        note = _window_note("pmc_sq_pview.json", w, window)
+        return {"note": note} if note else None
     try:
-        insts = json.load(open(prof))["counters"]["SQ_INSTS_VALU"]["per_launch"]
+        insts = d["counters"]["SQ_INSTS_VALU"]["per_launch"]
+        salu = d["counters"].get("SQ_INSTS_SALU", {}).get("per_launch")
     except Exception:
         return None
     per_cycle = insts / (1024 * 2.4e9 * kern_ms * 1e-3)
-    return {"bound": "valu-issue", "insts_per_launch": insts, "insts_per_simd_cycle": per_cycle,
-            "frac_of_2cycle_issue": per_cycle * 2.0, "clock_ghz": 2.4}
+    return {"bound": "valu-issue", "insts_per_launch": insts, "salu_insts_per_launch": salu,
+            "insts_per_simd_cycle": per_cycle, "frac_of_2cycle_issue": per_cycle * 2.0,
+            "clock_ghz": 2.4, "window_ticks": w}
 
 
 EVENT_CAP = 1 << 27          # records per shard (1 GB): config 3 records 70.7 M joins + removes
@@ -446,18 +479,17 @@ def event_summary(eng, nodes, last_tick, dist, crash):
             "full_detection_latency_ticks": stat((last - crash)[det])}
 
 
-def summarize_full(r, nodes, steps, world):
+def summarize_full(r, nodes, steps, world, warmup):
     achieved = r["bytes_per_tick"] / (r["kern_ms"] * 1e-3) / 1e9     # summed over ranks
     peak = PEAK_HBM_GBS * world
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if nodes == N_NODES and world == 1 and os.path.exists(prof):
-        try:
-            t = json.load(open(prof))
-            if t.get("launches_per_tick", 1) == r["tiles"]:
-                traffic = t.get("bytes_per_tick", t.get("bytes_per_launch"))
-        except Exception:
-            traffic = None
+    traffic = traffic_note = None
+    window = [warmup + 1, warmup + steps]
+    if nodes == N_NODES and world == 1:
+        t, w = _pmc("pmc_traffic.json", window)
+        if t is not None and t.get("launches_per_tick", 1) == r["tiles"]:
+            traffic = t.get("bytes_per_tick", t.get("bytes_per_launch"))
+        elif t is None:
+            traffic_note = _window_note("pmc_traffic.json", w, window)
     cfg = "config3" if nodes == N_NODES else "config4" if nodes == 262144 else "full view"
     return {
         "metric": "gossip node-rounds/sec (+ merge-kernel HBM GB/s, % peak)",
@@ -473,7 +505,9 @@ def summarize_full(r, nodes, steps, world):
         "merges_per_s": r["merges"] / r["el"],
         "xgmi_bytes_per_tick": r["xgmi_tick"], "xgmi_bytes_source": XGMI_SOURCE,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
-                     "frac": achieved / peak, "traffic": traffic, "kernel": "scale_tick_kernel",
+                     "frac": achieved / peak, "traffic": traffic, "window_ticks": window,
+                     **({"traffic_note": traffic_note} if traffic_note else {}),
+                     "kernel": "scale_tick_kernel",
                      "kernel_ms_per_tick": r["kern_ms"], "launches_per_tick": r["tiles"],
                      "kernel_ms_per_launch": r["kern_ms"] / r["tiles"],
                      ("exchange_csr_ms" if r["layout"] == "rows" else "csr_ms"): r["csr_ms"],
@@ -524,7 +558,7 @@ def main(argv=None):
     full = run_full(args.nodes, args.steps, args.warmup, world, local, dist)
     out = None
     if rank == 0:
-        out = summarize_full(full, args.nodes, args.steps, world)
+        out = summarize_full(full, args.nodes, args.steps, world, args.warmup)
         out.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                     "higher_is_better": True, "vs_baseline": None})
         if world == 1 and not args.no_cpu_baseline:
@@ -594,18 +628,18 @@ def main(argv=None):
         # (the table pair is 2 x 128 GiB of the 288 GB HBM), at N > 1 32 / N tiles per rank
         item("full262k", lambda: summarize_full(
             run_full(262144, min(args.steps, 8), 2, world, local, dist), 262144,
-            min(args.steps, 8), world))
+            min(args.steps, 8), world, 2))
     if world > 1 and not args.no_rows:
         # the full view ROW-sharded (north star: sender rows cross shards over RCCL send/recv,
         # deduplicated per (sender, shard)); O(f n^2) xGMI bytes per tick against the column
         # layout's O(n), reported beside it (DESIGN.md "Multi-GPU")
         item("full_rows", lambda: summarize_full(
             run_full(args.nodes, min(args.steps, 8), 2, world, local, dist, layout="rows"),
-            args.nodes, min(args.steps, 8), world), "config3")
+            args.nodes, min(args.steps, 8), world, 2), "config3")
         if not args.no_262k:
             if world >= 4:
                 item("full_rows", lambda: summarize_full(
-                    run_full(262144, 4, 2, world, local, dist, layout="rows"), 262144, 4, world),
+                    run_full(262144, 4, 2, world, local, dist, layout="rows"), 262144, 4, world, 2),
                     "config4")
             else:
                 # 2 x 68.7 GB of table rows plus ~2 x 66 GB of send/receive rows per GPU

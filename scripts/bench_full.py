@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     r = run_full(a.nodes, a.steps, a.warmup, 1, 0, None)
-    print(json.dumps(dict(summarize_full(r, a.nodes, a.steps, 1), steps=a.steps, warmup=a.warmup)),
+    print(json.dumps(dict(summarize_full(r, a.nodes, a.steps, 1, a.warmup), steps=a.steps, warmup=a.warmup)),
           flush=True)
 
 

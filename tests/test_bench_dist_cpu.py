@@ -139,3 +139,24 @@ def test_bench_two_ranks_gloo():
     pe = pv["events"]                                 # the partial view's removes-only run
     assert "error" not in pe, pe
     assert pe["kinds"] == 4 and pe["crashed_nodes_detected"] == 2 and pe["kernel_overhead_frac"] == 0.0
+
+
+def test_counter_fields_only_for_their_window():
+    """Committed PMC summaries cover ticks 6-25 (the driver's --steps 20 --warmup 5): a run over
+    that window prints them, any other window prints null with the window they belong to and
+    no VALU fraction."""
+    import bench
+    t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 25])
+    assert t is not None and note is None
+    t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 45])
+    assert t is None and "ticks 6-25" in note and "ticks 6-45" in note
+    v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 25])
+    assert v["frac_of_2cycle_issue"] > 0 and v["window_ticks"] == [6, 25]
+    v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 35])
+    assert set(v) == {"note"}
+    r = {"bytes_per_tick": 4.2e10, "kern_ms": 6.5, "rounds": 1, "el": 1.0, "merges": 1,
+         "xgmi_tick": 0.0, "layout": "columns", "tiles": 8, "csr_ms": 0.1}
+    out = bench.summarize_full(r, bench.N_NODES, 20, 1, 5)
+    assert out["roofline"]["traffic"] is not None
+    out = bench.summarize_full(r, bench.N_NODES, 40, 1, 5)
+    assert out["roofline"]["traffic"] is None and "ticks 6-45" in out["roofline"]["traffic_note"]
