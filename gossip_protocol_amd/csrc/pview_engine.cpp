@@ -39,7 +39,9 @@ struct PvShard {
     gsp::DevBuf<uint64_t> table[2];
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, out_pos, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok,
-        rows_run;                // tests (GSP_TEST_PV_COUNT_ROWS=1): rows run per tick
+        rows_run,                // tests (GSP_TEST_PV_COUNT_ROWS=1): rows run per tick
+        long_list;               // drain-all: [1 + rows] the rows sent > kPvMaxInbox messages
+    gsp::DevBuf<uint32_t> scratch;     // drain-all: the drain kernel's HBM lists
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     gsp::EvRing ev;
@@ -49,8 +51,9 @@ struct PvShard {
         for (int b = 0; b < 2; ++b) { table[b].release(); len[b].release(); }
         for (auto *b : {&own_hb, &fail_tick, &out_dst, &out_pos, &deg, &off, &fill, &csr_src, &err,
                         &tile_sum, &rc_info, &rc_src, &rc_slot, &kcount, &order, &start_tick, &ping,
-                        &joiners, &join_ok, &rows_run})
+                        &joiners, &join_ok, &rows_run, &long_list})
             b->release();
+        scratch.release();
         intro_buf.release();
         x.release();
         dig.release();
@@ -90,6 +93,10 @@ struct gsp_pview {
                                  // asynchronously every tick (they size the next tick's grids)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
+    bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
+    int32_t drain_grid = 0;      // drain kernel workgroups: 2 per CU (64 KB of LDS each)
+    int64_t scratch_cap = 0;     // drain kernel: entries per HBM list
+    int32_t drain_lds = 8192;    // drain kernel: LDS list capacity (GSP_TEST_PV_DRAIN_LDS lowers it)
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail, h_start;
@@ -120,7 +127,7 @@ struct gsp_pview {
         a.remote = rowmode ? sh.x.recv_rows.p : nullptr;
         a.n = p.n;
         a.view = p.view;
-        a.inbox = p.inbox;
+        a.inbox = p.inbox ? p.inbox : gsp::kPvMaxInbox;
         a.fanout = p.fanout;
         a.tick = t;
         a.tremove = p.tremove;
@@ -161,6 +168,17 @@ struct gsp_pview {
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
+        if (drain) {
+            a.drain = 1;
+            a.long_list = sh.long_list.p;
+            a.csr_off = sh.off.p;
+            a.csr_src = sh.csr_src.p;
+            a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
+            a.scratch = sh.scratch.p;
+            a.scratch_cap = scratch_cap;
+            a.drain_grid = drain_grid;
+            a.drain_lds = drain_lds;
+        }
         return a;
     }
 
@@ -171,7 +189,7 @@ struct gsp_pview {
         a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
         a.rows = sh.rows;
         a.row0 = sh.row0;
-        a.inbox = p.inbox;
+        a.inbox = p.inbox ? p.inbox : gsp::kPvMaxInbox;
         a.tick = tick + 1;
         a.max_segment = max_segment;
         a.rc_info = sh.rc_info.p;
@@ -180,6 +198,8 @@ struct gsp_pview {
         a.kcount = sort_rows ? sh.kcount.p : nullptr;
         a.order = sort_rows ? sh.order.p : nullptr;
         a.err = local[0].err.p;
+        a.drain = drain ? 1 : 0;
+        a.long_list = drain ? sh.long_list.p : nullptr;
         return a;
     }
 
@@ -197,8 +217,11 @@ int pview_validate(const gsp_pview_params *p) {
     GSP_REQUIRE(p->n >= 2 && p->n < (1 << 21), GSP_ERR_INVALID, "n=%d outside [2, 2^21 - 1]", p->n);
     GSP_REQUIRE(p->view >= 1 && p->view <= gsp::kPvMaxView, GSP_ERR_INVALID, "view=%d outside [1, %d]",
                 p->view, gsp::kPvMaxView);
-    GSP_REQUIRE(p->inbox >= 1 && p->inbox <= gsp::kPvMaxInbox, GSP_ERR_INVALID,
-                "inbox=%d outside [1, %d]", p->inbox, gsp::kPvMaxInbox);
+    GSP_REQUIRE(p->inbox >= 0 && p->inbox <= gsp::kPvMaxInbox, GSP_ERR_INVALID,
+                "inbox=%d outside [0, %d] (0: every message merged)", p->inbox, gsp::kPvMaxInbox);
+    GSP_REQUIRE(p->inbox > 0 || (p->tfail == 0 && p->swim == 0 && p->policy.intro_list == 0),
+                GSP_ERR_INVALID, "inbox=0 (drain all) runs the plain protocol (and join schedules "
+                "without an introducer list): tfail, swim and intro_list must be 0");
     GSP_REQUIRE(p->fanout >= 1 && p->fanout <= 16, GSP_ERR_INVALID, "fanout=%d outside [1,16]",
                 p->fanout);
     GSP_REQUIRE(p->tremove >= 1 && p->tremove <= 31, GSP_ERR_INVALID, "tremove=%d outside [1,31]",
@@ -266,6 +289,11 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
         if (s->rowmode && sh.row0 != 0) GSP_HIP(sh.intro_buf.alloc(size_t(V)));
     }
     if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
+    if (s->drain) {
+        GSP_HIP(sh.long_list.alloc(rows + 1));
+        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 4, st));
+        GSP_HIP(sh.scratch.alloc(size_t(s->drain_grid) * 4 * size_t(s->scratch_cap)));
+    }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
     if (const char *cr = std::getenv("GSP_TEST_PV_COUNT_ROWS"); cr && std::atoi(cr)) {
@@ -412,6 +440,17 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
+    s->drain = p->inbox == 0;
+    if (s->drain) {
+        // two 64 KB-LDS workgroups per CU; each holds an HBM list pair for the rows whose list
+        // outgrows LDS: a power of two >= n (a list holds distinct ids, a segment distinct
+        // senders), at most 2^19 entries (the job stops past it, GSP_ERR_CAPACITY)
+        s->drain_grid = 2 * s->cus;
+        s->scratch_cap = 8192;
+        while (s->scratch_cap < p->n && s->scratch_cap < (int64_t(1) << 19)) s->scratch_cap <<= 1;
+        if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
+            s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(8192, std::atoi(dl)));
+    }
     s->pos_scatter = !s->rowmode && !s->joins;
     if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
@@ -420,8 +459,9 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         max_rows = std::max(max_rows, gsp::rowx_row0(g + 1, p->n, shards) - gsp::rowx_row0(g, p->n, shards));
     s->pair_cap = max_rows;                       // a sender row goes to a shard at most once
     s->msg_cap = int64_t(max_rows) * p->fanout;
-    // the per-row overflow field of the digest record is 16 bits: k_all - k <= 65535
-    s->max_segment = std::min(gsp::kPvMaxSegment, 65535 + p->inbox);
+    // the per-row overflow field of the digest record is 16 bits: k_all - k <= 65535 (drain
+    // all: no overflow, no bound -- a long row's counts go to the digest directly)
+    s->max_segment = s->drain ? INT32_MAX : std::min(gsp::kPvMaxSegment, 65535 + p->inbox);
     if (const char *ms = std::getenv("GSP_TEST_MAX_SEGMENT"))   // tests only: force overflows
         s->max_segment = std::max(1, std::min(s->max_segment, std::atoi(ms)));
     GSP_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
@@ -562,6 +602,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         if (int rc = pv_join_scatter(s, t)) return rc;
         for (PvShard &sh : s->local) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
+            if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 4, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
             if (s->h_kseen)          // never waited on: the next ticks' grid predictions
                 GSP_HIP(hipMemcpyAsync(s->h_kseen + 8 * (&sh - s->local.data()), sh.kcount.p, 8 * 4,

@@ -42,6 +42,7 @@
 #include "join_kernels.hpp"
 #include "philox.hpp"
 #include "pview_kernels.hpp"
+#include "pview_rules.hpp"
 #include "scale_kernels.hpp"
 #include "wave_ops.hpp"
 
@@ -54,37 +55,6 @@ constexpr int kMaxKeys = kSlots * kMaxBlocks;         // 2048
 constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: above every node id
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
 static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
-
-// Event digest term (oracle/pview_oracle.c gsp_pv_event_mix): S + g(x) per event, S a row seed
-// per kind (1 join, 2 remove, 3 evict) and g(x) = ((x ^ lo32(S)) * 0x9E3779B1) >> 5.  A row
-// hashes ~1000 events per tick, so the per-event part is one multiply (round 4; it was a
-// three-multiply 64-bit finaliser): lanes sum g(x) in 32 bits (< 2^27 each, at most 30 per
-// lane) and pv_finish adds the S terms once per wave, as the wave's event counts times S.
-__device__ inline uint64_t pv_seed(uint32_t kind, uint32_t t, uint32_t r) {
-    uint64_t z = (uint64_t(kind) << 62) | (uint64_t(t & 0xFFFFF) << 42) | (uint64_t(r & 0x1FFFFF) << 21);
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__device__ inline uint32_t pv_hash(uint32_t s, uint32_t x) {
-    return ((x ^ s) * 0x9E3779B1u) >> 5;
-}
-
-// the reference's merge of one payload entry (packed hb << 5 | ts5, 0 = absent)
-__device__ inline uint32_t pv_merge(uint32_t e, uint32_t v, uint32_t t5, uint32_t tr) {
-    const uint32_t upd = ((v >> 5) > (e >> 5)) ? ((v & 0xFFE0u) | t5) : e;
-    const uint32_t add = (v != 0u && ((t5 - v) & 31u) < tr) ? v : 0u;
-    return e ? upd : add;
-}
-// eviction order bin of a surviving entry: age * 32 + min(h0 + t - age - hb, 31), th0 = h0 + t
-__device__ inline uint32_t pv_bin(uint32_t v, uint32_t t5, uint32_t th0) {
-    const uint32_t age = (t5 - v) & 31u;
-    const int32_t e = int32_t(th0 - age) - int32_t(v >> 5);
-    return (age << 5) | uint32_t(e < 0 ? 0 : e > 31 ? 31 : e);
-}
-// the sender entry of a GOSSIP: hb + 1 and ts = t, or (1, t) when absent (MP1Node.cpp:237-243)
-__device__ inline uint32_t pv_event(uint32_t v, uint32_t t5) { return (((v >> 5) + 1u) << 5) | t5; }
 
 // threadIdx.x as a value the compiler cannot see through: the persistent split kernels loop
 // over rows, and every lane-position value derived from the thread index (slot offsets, LDS
@@ -919,6 +889,9 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
     constexpr int SL = kSlots / NT;
     const int32_t tid = pv_tid<NT>(), lane = tid & 63;
     const int32_t r = a.row0 + lr;
+    // drain-all: a row sent more than kPvMaxInbox messages is pview_drain_kernel's (only the
+    // one-kernel form without row order reaches it here)
+    if (a.drain && (a.rc_info[lr] >> 3) > kPvMaxInbox) return;
     if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);     // tests: each row exactly once
     uint64_t ent0[SL];
 #pragma unroll
@@ -1036,6 +1009,12 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
 template <int kExt>
 __global__ void __launch_bounds__(kPvBlock, 8) pview_tick_kernel(PviewTickArgs a) {
     __shared__ PvShared<kMaxKeys> sh;
+    if (a.order && a.drain) {                // the bucketed rows only (drain: long rows are not)
+        int32_t total = 0;
+#pragma unroll
+        for (int q = 0; q <= kPvMaxInbox; ++q) total += a.kcount[q];
+        if (int32_t(blockIdx.x) >= total) return;
+    }
     pv_row<kExt, kPvBlock, 0, 7>(a, sh, pv_row_of(a, int32_t(blockIdx.x)));
 }
 
@@ -1163,14 +1142,25 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
     int32_t bs[8], bl[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) { bs[q] = 0x7FFFFFFF; bl[q] = 0; }
-    bool wide = false;
+    bool wide = false, lng = false;
     if (valid) {
         o0 = a.off[lr];
         k_all = a.off[lr + 1] - o0;
         if (k_all > a.max_segment) atomicCAS(a.err, 0, a.tick);   // this tick's tick kernel runs no row
+        else if (a.drain && k_all > kPvMaxInbox) lng = true;        // pview_drain_kernel's
         else if (k_all > kPvWaveSegment) wide = true;
         else pv_best8_scan(a, o0, 0, k_all, 1, bs, bl);
-        k = k_all > a.max_segment ? 0 : (k_all < a.inbox ? k_all : a.inbox);
+        k = (k_all > a.max_segment || lng) ? 0 : (k_all < a.inbox ? k_all : a.inbox);
+    }
+    if (a.drain) {           // the long rows of this wave: one atomic per wave
+        const unsigned long long lm = __ballot(lng);
+        if (lm) {
+            const int32_t lane0 = __builtin_ffsll(lm) - 1;
+            int32_t base = 0;
+            if (lane == lane0) base = atomicAdd(&a.long_list[0], __popcll(lm));
+            base = __shfl(base, lane0, 64);
+            if (lng) a.long_list[1 + base + __popcll(lm & ((1ull << lane) - 1ull))] = lr;
+        }
     }
     // the wave's wide rows, one after the other (wave-uniform loop)
     for (unsigned long long m = __ballot(wide); m; m &= m - 1) {
@@ -1208,12 +1198,13 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
         __shared__ int32_t s_cnt[8], s_base[8];
         if (threadIdx.x < 8) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        const int32_t pos = valid ? atomicAdd(&s_cnt[k], 1) : 0;
+        const bool bucket = valid && !lng;       // drain: a long row is in no bucket
+        const int32_t pos = bucket ? atomicAdd(&s_cnt[k], 1) : 0;
         __syncthreads();
         if (threadIdx.x < 8 && s_cnt[threadIdx.x])
             s_base[threadIdx.x] = atomicAdd(&a.kcount[threadIdx.x], s_cnt[threadIdx.x]);
         __syncthreads();
-        if (valid) a.order[int64_t(k) * a.rows + s_base[k] + pos] = lr;
+        if (bucket) a.order[int64_t(k) * a.rows + s_base[k] + pos] = lr;
     }
 }
 
@@ -1487,6 +1478,10 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
 #undef GSP_PV_K5
 #undef GSP_PV_K4
 #undef GSP_PV_K03
+        if (a.drain) {
+            const hipError_t e = launch_pview_drain(b, st);
+            if (e != hipSuccess) return e;
+        }
         launch_send_and_digest(b, st);
         return hipGetLastError();
     }
@@ -1496,6 +1491,10 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         case kExtPol: hipLaunchKernelGGL((pview_tick_kernel<kExtPol>), g, blk, 0, st, a); break;
         case kExtPol | kExtEv: hipLaunchKernelGGL((pview_tick_kernel<kExtPol | kExtEv>), g, blk, 0, st, a); break;
         default: hipLaunchKernelGGL((pview_tick_kernel<kExtRot | kExtPol | kExtEv>), g, blk, 0, st, a); break;
+    }
+    if (a.drain) {
+        const hipError_t e = launch_pview_drain(a, st);
+        if (e != hipSuccess) return e;
     }
     launch_send_and_digest(a, st);
     return hipGetLastError();

@@ -78,6 +78,17 @@ struct PviewTickArgs {
     int32_t *rows_run;           // tests only (GSP_TEST_PV_COUNT_ROWS=1): [1] counter of this
                                  // tick, +1 per row a tick kernel runs (every row exactly once,
                                  // in every launch form), or null
+    // drain-all (gsp_pview_params.inbox = 0, pview_drain.hip): a row sent more than
+    // kPvMaxInbox messages is listed by the receipt kernel and merges them all there
+    int32_t drain;               // 1: inbox 0 (the tick kernels skip the listed rows)
+    const int32_t *long_list;    // [1 + rows]: count, then the listed rows
+    const int32_t *csr_off;      // [rows + 1] this tick's receiver CSR
+    int32_t *csr_src, *csr_slot; // its senders (sorted in place) and rows (row mode, or null)
+    uint32_t *scratch;           // [drain_grid][4][scratch_cap]: HBM lists of long rows
+    int64_t scratch_cap;         // entries per list (>= the LDS capacity, a power of two)
+    int32_t drain_grid;          // drain kernel workgroups (persistent)
+    int32_t drain_lds;           // LDS list / segment-sort capacity in use (tests lower it to
+                                 // reach the HBM paths, GSP_TEST_PV_DRAIN_LDS), <= 8192
 };
 constexpr int kPvProfPhases = 16;   // per (slot, k): phases 0..14, rows sampled
 
@@ -89,12 +100,16 @@ struct PviewReceiptArgs {
     int32_t *rc_info, *rc_src, *rc_slot;
     int32_t *kcount, *order;     // k-bucketed row order for the tick kernel (or null)
     int32_t *err;
+    int32_t drain;               // inbox 0: rows sent more than kPvMaxInbox messages go to
+    int32_t *long_list;          // long_list ([1 + rows], count first), not into the buckets
 };
 
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st);
 hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st);
 // tick kernel, then the send kernel (peers, drops) and the digest reduction
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st);
+// drain-all rows (a.drain): launched by launch_pview_tick after the tick kernels
+hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st);
 // receiver CSR of one shard from the send kernel's positions: csr_src[off[d] + pos] = sender
 hipError_t launch_pview_scatter(const int32_t *out_dst, const int32_t *out_pos, int64_t slots,
                                 int32_t fanout, const int32_t *off, int32_t *csr_src, hipStream_t st);

@@ -481,9 +481,12 @@ int gsp_events_write_log(uint64_t *ev, int64_t n, const char *path);
 
 /* ------------------------------------------------------------------------------------
  * PARTIAL-VIEW engine (BASELINE config 5): every node keeps at most `view` member entries
- * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (ascending
- * sender; the rest are counted as overflow); after the TREMOVE scan a view larger than
- * `view` keeps the entries with the smallest (age, -hb, id).  DESIGN.md "Partial view".
+ * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (1..7,
+ * ascending sender; the rest are counted as overflow) -- or, with inbox = 0, every message it
+ * was sent, as the reference's checkMessages drains its queue (MP1Node.cpp:200-212; the plain
+ * protocol and join schedules without an introducer list: tfail, swim and intro_list 0);
+ * after the TREMOVE scan a view larger than `view` keeps the entries with the smallest
+ * (age, -hb, id).  DESIGN.md "Partial view".
  * ---------------------------------------------------------------------------------- */
 typedef struct gsp_pview gsp_pview;
 

@@ -142,7 +142,7 @@ typedef struct {
     int32_t n;          /* nodes                                                    */
     int32_t view;       /* V: entries kept per node                                 */
     int32_t fanout;
-    int32_t inbox;      /* K: messages merged per node per tick (rest = overflow)   */
+    int32_t inbox;      /* K: messages merged per node per tick (rest = overflow); 0: all */
     int32_t drop_pct, tremove, h0, fail_mode, fail_tick, fail_ppm;
     uint64_t seed;
     int32_t tfail, swim;   /* as gsp_scale_cfg */

@@ -8,7 +8,8 @@
  *   init      view of r = {(r + 1 + j * (n / V)) mod n : j < V} (all others if n - 1 <= V),
  *             hb = h0, ts = 0 -- among the nodes that start at tick 0;
  *   inbox     a receiver merges at most K messages per tick, in ascending sender order; the
- *             rest are counted as overflow and ignored;
+ *             rest are counted as overflow and ignored.  K = 0 drains every message, as the
+ *             reference's checkMessages does (MP1Node.cpp:200-212);
  *   evict     after the TREMOVE scan, a view larger than V keeps the V entries with the
  *             smallest (age, -hb, id);
  *   send      min(f, cnt) distinct members by Philox rank-select over the id order of the
@@ -163,7 +164,7 @@ static void pv_send_all(gsp_pview_oracle *o, int tab, int32_t t, gsp_pview_diges
 
 gsp_pview_oracle *gsp_pview_oracle_create(const gsp_pview_cfg *cfg) {
     if (!cfg || cfg->n < 2 || cfg->view < 1 || cfg->fanout < 1 || cfg->fanout > 60 ||
-        cfg->inbox < 1 || cfg->swim < 0 || cfg->swim > 8 || cfg->pol.intro_list < 0 ||
+        cfg->inbox < 0 || cfg->swim < 0 || cfg->swim > 8 || cfg->pol.intro_list < 0 ||
         cfg->pol.intro_list > 16)
         return NULL;
     gsp_pview_oracle *o = calloc(1, sizeof *o);
@@ -339,7 +340,7 @@ int32_t gsp_pview_oracle_row_step(const gsp_pview_cfg *c, int32_t t, int32_t r,
                                   const int32_t *sv_hb, const int32_t *sv_ts,
                                   const int32_t *sv_len, int32_t *out_id, int32_t *out_hb,
                                   int32_t *out_ts, gsp_pview_digest *d) {
-    const int32_t V = c->view, K = c->inbox;
+    const int32_t V = c->view, K = c->inbox ? c->inbox : nsend;   /* 0: drain every message */
     if (nsend < 0 || own_len < 0 || own_len > V) return -1;
     int32_t *order = malloc(sizeof(int32_t) * (nsend ? nsend : 1));
     for (int32_t j = 0; j < nsend; ++j) order[j] = j;
@@ -429,7 +430,7 @@ int32_t gsp_pview_oracle_remove_scan(int32_t t, int32_t T, int32_t *id, int32_t 
 
 int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
     const gsp_pview_cfg *c = &o->c;
-    const int32_t n = c->n, V = c->view, K = c->inbox;
+    const int32_t n = c->n, V = c->view;
     const int32_t t = o->t + 1;
     const int prev = o->cur, next = 1 - o->cur;
     memset(d, 0, sizeof *d);
@@ -439,7 +440,10 @@ int gsp_pview_oracle_step(gsp_pview_oracle *o, gsp_pview_digest *d) {
 
     int32_t *deg = calloc((size_t)n + 1, sizeof(int32_t));
     for (int64_t m = 0; m < o->nmsg; ++m) deg[o->mdst[m] + 1]++;
+    int32_t kmax = 0;                    /* the largest segment: K = 0 merges all of it */
+    for (int32_t r = 0; r < n; ++r) kmax = deg[r + 1] > kmax ? deg[r + 1] : kmax;
     for (int32_t r = 0; r < n; ++r) deg[r + 1] += deg[r];
+    const int32_t K = c->inbox ? c->inbox : (kmax > 0 ? kmax : 1);
     int32_t *fill = calloc(n, sizeof(int32_t));
     int32_t *bucket = malloc(sizeof(int32_t) * (o->nmsg ? o->nmsg : 1));
     for (int64_t m = 0; m < o->nmsg; ++m) {

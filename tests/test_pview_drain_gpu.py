@@ -1,0 +1,147 @@
+"""Drain-all partial view (gsp_pview_params.inbox = 0) on the GPU against oracle/pview_oracle.c.
+
+The reference drains every queued message (checkMessages, MP1Node.cpp:200-212); with inbox = 0
+so does the partial view: rows sent at most 7 messages run in the tick kernels, rows sent more
+run in pview_drain_kernel (gossip_protocol_amd/csrc/pview_drain.hip), which merges them all in
+ascending sender order.  Every tick's digest (no overflow), the message lists and the views must
+equal the oracle's, which folds every message of every row the same way.  The cases make most
+rows long (fan-out 8 and 16 against small views), make hubs past 1,000 senders (a join burst
+of 2,000 nodes knowing only the introducer), and force the drain kernel's HBM paths (a list or
+segment past its LDS capacity, GSP_TEST_PV_DRAIN_LDS lowers it).
+"""
+import numpy as np
+import pytest
+
+from gossip_protocol_amd.pview import PviewEngine, unpack_view
+from tests.oracle_binding import PviewOracle, make_policy as oracle_policy
+from gossip_protocol_amd._lib import make_policy
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp_rows(eng, orc, rows, t):
+    for r in rows:
+        ids_o, hb_o, ts_o = orc.row(r)
+        buf, ln = eng.row(r)
+        ids, hb, ts5 = unpack_view(buf, ln)
+        assert ln == len(ids_o), "tick %d len row %d: %d vs %d" % (t, r, ln, len(ids_o))
+        assert np.array_equal(ids, ids_o), "tick %d ids row %d" % (t, r)
+        assert np.array_equal(hb, hb_o), "tick %d hb row %d" % (t, r)
+        assert np.array_equal(ts5, ts_o & 31), "tick %d ts row %d" % (t, r)
+        assert np.all(buf[ln:] == np.uint64(0xFFFFFFFFFFFFFFFF))
+        if orc.fail_tick(r) >= t:
+            assert eng.own_hb(r) == orc.own_hb(r), "own hb row %d" % r
+
+
+def _run(n, ticks, kw, policy=None, events=False, rows_run=False, group=1, every=1, check=None):
+    from gossip_protocol_amd import _lib
+    orc = PviewOracle(n, policy=oracle_policy(**policy) if policy else None, **kw)
+    ekw = dict(kw)
+    if policy:
+        ekw["policy"] = make_policy(**policy)
+    longest = 0
+    rng = np.random.default_rng(kw.get("seed", 1))
+    with PviewEngine(n, max_ticks=ticks, events=events, group=group, **ekw) as eng:
+        if events:
+            eng.drain_events()
+        for t in range(1, ticks + 1):
+            src, dst = orc.messages()                    # sent at t - 1, merged at t
+            if len(dst):
+                longest = max(longest, int(np.bincount(dst, minlength=n).max()))
+            want = orc.step()
+            eng.step(1)
+            got = eng.digest(t)
+            assert got == want, "tick %d\n got %s\nwant %s" % (t, got, want)
+            assert got["overflow"] == 0
+            if rows_run:
+                assert eng.rows_run(t) == n, "tick %d: %d rows run" % (t, eng.rows_run(t))
+            if events:
+                rec, lost = eng.drain_events()
+                assert lost == 0
+                k, tk, r, x = _lib.split_events(rec)
+                ok, orr, ox = orc.events()
+                assert sorted(zip(k.tolist(), r.tolist(), x.tolist())) == \
+                    sorted(zip(ok.tolist(), orr.tolist(), ox.tolist())), "events tick %d" % t
+            if t % every == 0 or t == ticks:
+                m = eng.messages()
+                src, dst = orc.messages()
+                assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+                    sorted(zip(src.tolist(), dst.tolist())), "messages tick %d" % t
+                rows = sorted(set(rng.integers(0, n, 60).tolist()) | set(check or ()))
+                _cmp_rows(eng, orc, rows, t)
+    return longest
+
+
+CASES = [
+    # n, view, fanout, drop, fail_mode, fail_tick, ppm, seed, ticks
+    (3000, 32, 8, 0, 1, 5, 20000, 3, 24),        # most rows sent > 7 messages
+    (2000, 64, 3, 10, 2, 8, 50000, 7, 30),       # config-5 rules: a few long rows
+    (4096, 16, 16, 10, 1, 6, 10000, 5, 16),      # full fan-out to a 16-entry view: k ~ 14
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d" % c[:3])
+def test_drain_all_matches_oracle(case):
+    n, V, f, drop, mode, ftick, ppm, seed, ticks = case
+    kw = dict(view=V, fanout=f, inbox=0, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
+              fail_ppm=ppm, seed=seed)
+    longest = _run(n, ticks, kw, every=4)
+    assert longest > 7
+
+
+@pytest.mark.parametrize("evict_order", [0, 1])
+def test_drain_all_events_and_rows_run(monkeypatch, evict_order):
+    """Every join / remove / evict record of the long rows, every row run exactly once (the
+    split kernels skip the long rows; the drain kernel runs them)."""
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=30000,
+              seed=17, tremove=10, evict_order=evict_order)
+    _run(2500, 20, kw, events=True, rows_run=True, every=5)
+
+
+@pytest.mark.parametrize("form", ["0:1", "1:1", "0:0"])
+def test_drain_all_kernel_forms(monkeypatch, form):
+    """The one-kernel form (GSP_PV_SPLIT=0) with and without row order (GSP_PV_SORT): a long
+    row reaches pview_tick_kernel there and must be left to the drain kernel."""
+    split, sort = form.split(":")
+    monkeypatch.setenv("GSP_PV_SPLIT", split)
+    monkeypatch.setenv("GSP_PV_SORT", sort)
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    kw = dict(view=32, fanout=8, inbox=0, drop_pct=0, fail_mode=2, fail_tick=5, fail_ppm=50000, seed=29)
+    _run(2000, 14, kw, rows_run=True, every=7)
+
+
+def test_drain_all_hbm_paths(monkeypatch):
+    """GSP_TEST_PV_DRAIN_LDS=300: a long row's list moves to the workgroup's HBM scratch once it
+    could pass 300 entries, and a segment of more than 256 senders is sorted in HBM."""
+    monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
+    kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=5, fail_ppm=20000, seed=31)
+    _run(3000, 16, kw, every=4)
+
+
+def test_drain_all_join_burst_past_1000_senders(monkeypatch):
+    """2,000 nodes start in one tick knowing only the introducer (no introducer list) and all
+    gossip to it: node 0 is sent more than 1,000 messages a tick and merges every one of them
+    (the inbox-7 engine drops all but 7); with a low LDS bound its list and its segment sort
+    also take the HBM paths."""
+    kw = dict(view=64, fanout=3, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=20000,
+              seed=43)
+    pol = dict(step_rate=0.0005, intro_list=0)
+    longest = _run(5000, 8, kw, policy=pol, every=2, check=range(0, 40))
+    assert longest > 1000, "node 0 must be sent more than 1,000 messages (got %d)" % longest
+    monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "1024")
+    assert _run(5000, 6, kw, policy=pol, every=3, check=range(0, 10)) > 1000
+
+
+def test_drain_all_row_shards():
+    """Row shards (in-process group of 3): the long rows' senders come from other shards' rows
+    (received views, csr_slot < 0)."""
+    kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=2, fail_tick=6, fail_ppm=50000, seed=37)
+    _run(2400, 14, kw, group=3, every=7)
+
+
+def test_drain_all_rejects_protocol_extensions():
+    from gossip_protocol_amd._lib import GspError
+    for extra in (dict(tfail=5), dict(swim=2)):
+        with pytest.raises(GspError, match="drain all"):
+            PviewEngine(500, view=32, inbox=0, max_ticks=2, **extra)

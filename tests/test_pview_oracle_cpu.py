@@ -63,3 +63,25 @@ def test_rotated_eviction_keeps_the_rotated_id_prefix():
         want = np.sort(tied[np.argsort((tied - m) % n, kind="stable")[:V - 1]])
         assert np.array_equal(np.setdiff1d(gi, [sender]), want), order
         assert d["evicts"] == len(tied) - (V - 1)
+
+
+def test_drain_all_is_an_unbounded_inbox():
+    """inbox = 0 drains every message (MP1Node.cpp:200-212): with every in-degree below 200 the
+    oracle at inbox 0 and at inbox 200 run the same protocol -- same digests (no overflow in
+    either), same views -- while inbox 2 discards messages and diverges."""
+    kw = dict(view=32, fanout=6, drop_pct=10, fail_mode=1, fail_tick=4, fail_ppm=30000, seed=5)
+    n = 800
+    a, b, c = (PviewOracle(n, inbox=k, **kw) for k in (0, 200, 2))
+    over = 0
+    for t in range(1, 13):
+        src, dst = a.messages()
+        assert np.bincount(dst, minlength=n).max() < 200
+        da, db, dc = a.step(), b.step(), c.step()
+        assert da == db and da["overflow"] == 0, t
+        over += dc["overflow"]
+    for r in range(0, n, 13):
+        for x, y in zip(a.row(r), b.row(r)):
+            assert np.array_equal(x, y)
+    assert over > 0
+    for o in (a, b, c):
+        o.close()

@@ -71,7 +71,7 @@ def test_facade_receive_paths_match_the_reference(tmp_path, conf, mode, seed):
     _need(GPU_DRIVER)
     want = _run(REF_DRIVER, str(tmp_path / "ref"), conf, mode, seed)
     got = _run(GPU_DRIVER, str(tmp_path / "gpu"), conf, mode, seed)
-    if mode not in ("wrapper", "inject"):                 # the callback modes see messages
+    if mode not in ("wrapper", "inject", "members"):      # the callback modes see messages
         assert b"messages=0 " not in want["stdout"]
     for name in OUTPUTS:
         if got[name] != want[name]:
