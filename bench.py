@@ -16,7 +16,10 @@ reductions (DESIGN.md "Multi-GPU").
 Second line item (`pview`): BASELINE config 5 -- 1,048,576 nodes, bounded partial view
 V = 256, fanout 3, inbox 7, 10% drops, 5% contiguous crash at t = 10; N > 1: row-sharded
 over N GPUs with the per-tick sender-view exchange over RCCL send/recv (strong scaling);
-reports its own node-rounds/s, tick-kernel roofline and xGMI bytes per tick.
+reports its own node-rounds/s, tick-kernel roofline and xGMI bytes per tick, the share of
+delivered messages the inbox bound discards (inbox_overflow_frac) and the share of removals
+that hit live nodes (removes_of_live_frac, from the event run).  `pview_drain`: the same
+workload with every message merged (inbox 0, as the reference drains its queue).
 Prints ONE JSON line (rank 0) with the roofline of the fused tick kernel and the CPU
 baseline (the oracle restatement, timed on a bounded sample of the same workload).
 """
@@ -182,14 +185,18 @@ def pview_cpu_baseline(budget_s=10.0):
             "sample": "oracle/pview_oracle.c, n=5000, V=256, %d ticks in %.1f s" % (ticks, el)}
 
 
-def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1, events=0):
+def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1, events=0,
+              inbox=None):
     """Config 5 on `world` GPUs (row shards).  Returns the rank-0 summary (None elsewhere).
     Algorithmic bytes per node-round: own view read + write (2 * V * 8) + one sender view per
     merged message (V * 8) + 4 B per CSR entry.  events: a kind mask (gsp_pview_params.events);
-    the summary is then the event one (event_summary) with the kernel time."""
+    the summary is then the event one (event_summary) with the kernel time.  inbox: 0 runs the
+    drain-all protocol (every message merged, gsp_pview_params.inbox = 0)."""
     import torch
     from gossip_protocol_amd.pview import PviewEngine
     kw = dict(PV_KW, max_ticks=warmup + steps)
+    if inbox is not None:
+        kw["inbox"] = inbox
     if events:
         kw.update(events=events, event_cap=EVENT_CAP)
     if dist is not None:
@@ -213,12 +220,13 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     el = time.perf_counter() - t0
     eng.sync()
     p1 = eng.perf()
-    rounds = delivered = merges = csr = 0
+    rounds = delivered = merges = csr = overflow = 0
     for t in range(warmup + 1, warmup + steps + 1):
         d = eng.digest(t)
         rounds += d["node_rounds"]
         delivered += d["delivered"]
         merges += d["merges"]
+        overflow += d["overflow"]
         csr += d["delivered"] + d["overflow"]
     V = PV_KW["view"]
     launches = max(p1["merge_launches"] - p0["merge_launches"], 1)
@@ -236,11 +244,11 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     if dist is not None:
         t = torch.tensor([el, kern_ms, xch_ms], dtype=torch.float64, device=_dev())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        u = torch.tensor([rounds, merges, bytes_per_tick, xgmi], dtype=torch.float64,
-                         device=_dev())
+        u = torch.tensor([rounds, merges, bytes_per_tick, xgmi, overflow, csr],
+                         dtype=torch.float64, device=_dev())
         dist.all_reduce(u, op=dist.ReduceOp.SUM)
         el, kern_ms, xch_ms = (x.item() for x in t)
-        rounds, merges, bytes_per_tick, xgmi = (x.item() for x in u)
+        rounds, merges, bytes_per_tick, xgmi, overflow, csr = (x.item() for x in u)
         if dist.get_rank() != 0:
             return None
     if events:
@@ -249,21 +257,28 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     achieved = bytes_per_tick / (kern_ms * 1e-3) / 1e9
     peak = PEAK_HBM_GBS * world
     window = [warmup + 1, warmup + steps]
-    traffic, traffic_note = _pview_traffic(nodes, world, window)
+    # the committed PMC passes are of the inbox-7 protocol: nothing for the drain-all run
+    headline = kw["inbox"] == PV_KW["inbox"]
+    traffic, traffic_note = _pview_traffic(nodes, world, window) if headline else (None, None)
+    k_in = kw["inbox"]
     out = {
         "metric": "gossip node-rounds/sec (partial view)", "value": rounds / el,
         "unit": "node-rounds/s", "ms_per_step": el * 1e3 / steps, "scaling": "strong",
         "dtype": "u64 entries (id:32 | hb:11 | ts:5)",
-        "config": {"workload": "config5: %d nodes, partial view V=256, fanout 3, inbox 7, 10%% "
-                               "drop, 5%% contiguous crash at t=10" % nodes,
+        "config": {"workload": "config5: %d nodes, partial view V=256, fanout 3, %s, 10%% "
+                               "drop, 5%% contiguous crash at t=10" %
+                               (nodes, "inbox %d" % k_in if k_in else "inbox 0 (drain all)"),
+                   "inbox": k_in,
                    "parallelism": ("rows%d" % world if world > 1 else
                                    "rows%d-in-process" % group if group > 1 else "1gpu")},
         "merges_per_s": merges / el,
+        # the share of delivered messages the bounded inbox discards (0 when draining all)
+        "inbox_overflow_frac": overflow / csr if csr else 0.0,
         "xgmi_bytes_per_tick": xgmi, "xgmi_bytes_source": XGMI_SOURCE, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
-                     "valu": _pview_valu(nodes, world, kern_ms, window),
+                     "valu": _pview_valu(nodes, world, kern_ms, window) if headline else None,
                      "window_ticks": window,
                      "kernel_ms_per_tick": kern_ms, "algorithmic_bytes_per_tick": bytes_per_tick},
     }
@@ -543,6 +558,8 @@ def main(argv=None):
                     help="skip the event-stream run (detection latency, recording cost)")
     ap.add_argument("--no-rows", action="store_true",
                     help="skip the full-view row-layout line items (N > 1)")
+    ap.add_argument("--no-drain", action="store_true",
+                    help="skip the drain-all config-5 line item (inbox 0)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -611,18 +628,31 @@ def main(argv=None):
     if not args.no_pview:
         item("pview", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world,
                                         local, dist, not args.no_cpu_baseline))
-    if not args.no_pview and not args.no_events:
+    def _pv_events(key, inbox=None):
         # the partial view records removes only: its joins and evictions are ~8e8 records per
-        # tick at config 5 (6.7 GB, more than the tick's state traffic; scripts/events_cost.py)
-        def _pv_events():
-            r = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
-                          False, events=4)
-            if r is not None and out is not None and isinstance(out.get("pview"), dict) \
-                    and "roofline" in out["pview"]:
-                k0 = out["pview"]["roofline"]["kernel_ms_per_tick"]
-                r.update(kernel_ms_events_off=k0, kernel_overhead_frac=r["kernel_ms"] / k0 - 1.0)
-            return r
-        item("pview", _pv_events, "events")
+        # tick at config 5 (6.7 GB, more than the tick's state traffic; scripts/events_cost.py).
+        # removes_of_live_frac: the share of removals whose node never crashed -- churn of the
+        # bounded view, not failure detection (the reference's grader fails any of them,
+        # Grader.sh:69-76)
+        r = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
+                      False, events=4, inbox=inbox)
+        if r is None:
+            return None
+        r["removes_of_live_frac"] = r["removes_of_live_nodes"] / r["removes"] if r["removes"] else 0.0
+        if out is not None and isinstance(out.get(key), dict) and "roofline" in out[key]:
+            k0 = out[key]["roofline"]["kernel_ms_per_tick"]
+            r.update(kernel_ms_events_off=k0, kernel_overhead_frac=r["kernel_ms"] / k0 - 1.0)
+            out[key]["removes_of_live_frac"] = r["removes_of_live_frac"]
+        return r
+    if not args.no_pview and not args.no_events:
+        item("pview", lambda: _pv_events("pview"), "events")
+    if not args.no_pview and not args.no_drain:
+        # config 5 with every delivered message merged (inbox 0), as the reference drains its
+        # queue (MP1Node.cpp:200-212): the cost of the protocol without the inbox bound
+        item("pview_drain", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup,
+                                              world, local, dist, False, inbox=0))
+        if not args.no_events:
+            item("pview_drain", lambda: _pv_events("pview_drain", inbox=0), "events")
     if not args.no_262k:
         # BASELINE config 4: 262,144 nodes full view, 8,192-column tiles: on one GPU 32 tiles
         # (the table pair is 2 x 128 GiB of the 288 GB HBM), at N > 1 32 / N tiles per rank

@@ -102,8 +102,7 @@ struct gsp_pview {
     std::vector<int32_t> h_fail, h_start;
     bool joins = false;          // a join schedule is set (some node starts after tick 0)
     gsp::JoinPlan plan;
-    int32_t *h_cnt = nullptr;    // pinned [G][2G + 1]: pair counts, record counts, capacity flag
-    int32_t *h_recv = nullptr;   // pinned [local][G]: records each local shard receives
+    gsp::RowxState rowx;         // row exchange: count ring, posted sizes (rowx_host.hpp)
     struct Timed { hipEvent_t a, b, c; };
     std::vector<Timed> pending;
     std::vector<hipEvent_t> free_events;
@@ -270,7 +269,7 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     }
     GSP_HIP(hipMemsetAsync(sh.rowdig.p, 0, rows * 16 * 8, st));
     if (s->rowmode)
-        GSP_HIP(sh.x.alloc(G, s->pair_cap, s->msg_cap, V, int64_t(n) * F, st));
+        GSP_HIP(sh.x.alloc(G, s->pair_cap, s->msg_cap, V, true, s->comm != nullptr, int64_t(n) * F, st));
     if (s->p.swim > 0) {
         GSP_HIP(sh.ping.alloc(rows));
         GSP_HIP(hipMemsetAsync(sh.ping.p, 0xFF, rows * 4, st));     // -1: no probe yet
@@ -315,8 +314,8 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
 // Move the sender views of tick t_sent's cross-shard messages to their destination shards and
 // build every local shard's receiver CSR for tick t_sent + 1 (rowx_host.cpp).
 int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
-    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, s->p.view, s->pair_cap, s->msg_cap,
-                     s->comm, s->st, s->h_cnt, s->h_recv};
+    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, s->p.view, true, s->pair_cap, s->msg_cap,
+                     s->comm, s->st, t_sent + 1, &s->rowx};
     std::vector<gsp::RowxShard> v;
     for (PvShard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p, sh.table[t_sent & 1].p,
@@ -331,10 +330,15 @@ int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
 // flag (shard 0's), so an in-process group stops as a whole; ranks of a communicator
 // exchange their flags with the row-exchange counts and stop at the same tick.
 int pview_mirrored_err(gsp_pview *s) {
-    for (size_t i = 0; i < s->local.size(); ++i)
-        GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
+    for (size_t i = 0; i < s->local.size(); ++i) {
+        const int32_t e = s->h_err[i];
+        GSP_REQUIRE(!(e & gsp::kRowxErrBit), GSP_ERR_CAPACITY,
+                    "row exchange at tick %d: a shard's rows or records passed the region capacity "
+                    "or the size posted to RCCL; the job stopped there", e & ~gsp::kRowxErrBit);
+        GSP_REQUIRE(e == 0, GSP_ERR_CAPACITY,
                     "a receiver was sent more than %d messages at tick %d; the job stopped there",
-                    s->max_segment, s->h_err[i]);
+                    s->max_segment, e);
+    }
     return GSP_OK;
 }
 
@@ -402,6 +406,8 @@ int pview_collect(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     s->pending.clear();
+    if (s->rowmode)
+        if (int rc = gsp::rowx_collect(s->rowx, &s->perf.xgmi_bytes)) return rc;
     for (size_t i = 0; i < s->local.size(); ++i)
         GSP_HIP(hipMemcpy(s->h_err + i, s->local[i].err.p, 4, hipMemcpyDeviceToHost));
     return pview_mirrored_err(s);
@@ -468,9 +474,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt),
-                              size_t(gsp::rowx_cnt_stride(shards)) * shards * 4));
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
+        GSP_HIP(s->rowx.init(shards, nccl_id != nullptr));
     }
     if (nccl_id) {
         ncclUniqueId id;
@@ -556,8 +560,7 @@ int gsp_pview_destroy(gsp_pview *s) {
         sh.release();
     }
     if (s->comm) (void)ncclCommDestroy(s->comm);
-    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
-    if (s->h_recv) (void)hipHostFree(s->h_recv);
+    s->rowx.release();
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->h_kcount) (void)hipHostFree(s->h_kcount);
     if (s->h_kseen) (void)hipHostFree(s->h_kseen);

@@ -1,14 +1,20 @@
 // gossip_protocol_amd/csrc/rowx_host.cpp -- the row-shard exchange, host side (rowx_host.hpp).
 //
-//   pack + gather    per local shard: pairs (sender, destination shard) and message records
-//   counts           all-gather of every shard's 2G counts; the host reads them (the one sync
-//                    per tick: RCCL needs element counts)
-//   rows + records   one ncclGroupStart/End of ncclSend/ncclRecv per peer (one process per
-//                    GPU), or device copies between the shards of an in-process group
-//   csr              received records -> deg, scan, local + remote scatter
+//   pack + gather    per local shard: pairs (sender, destination shard) and message records;
+//                    partial-view rows packed for the wire (rowx_kernels.hpp)
+//   counts           all-gather of every shard's 2G counts + capacity flag (device), copied to
+//                    pinned memory behind an event
+//   check            the counts against the capacities and the sizes posted; in-band receive
+//                    counts for every later kernel
+//   rows + records   one ncclGroupStart/End of ncclSend/ncclRecv per peer, sized from earlier
+//                    exchanges (one process per GPU), or device copies between the shards of an
+//                    in-process group, sized by the device counts
+//   unpack + csr     packed rows decoded; received records -> deg, scan, local + remote scatter
 #include "rowx_host.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "scale_kernels.hpp"
 
@@ -19,33 +25,97 @@ constexpr size_t kPiece = size_t(1) << 27;      // 8-byte words per ncclSend / n
 }
 
 hipError_t RowxBufs::alloc(int32_t shards, int64_t pair_cap, int64_t msg_cap, int32_t row_words,
-                           int64_t csr_cap, hipStream_t st) {
+                           bool packed, bool rccl, int64_t csr_cap, hipStream_t st) {
     const size_t G = size_t(shards), R = size_t(shards > 1 ? shards - 1 : 1);   // regions
+    const size_t wire = size_t(packed ? rowx_packed_words(row_words) : row_words);
     hipError_t e;
     const size_t S = size_t(rowx_cnt_stride(shards));
     if ((e = cnt.alloc(S)) != hipSuccess) return e;
     if ((e = cnt_all.alloc(S * G)) != hipSuccess) return e;
     if ((e = recv_msgs.alloc(G)) != hipSuccess) return e;
+    if ((e = recv_pairs.alloc(G)) != hipSuccess) return e;
+    if ((e = bounds.alloc(size_t(RowxState::kRing) * 2 * G * G)) != hipSuccess) return e;
     if ((e = pair_row.alloc(R * size_t(pair_cap))) != hipSuccess) return e;
     if ((e = csr_slot.alloc(size_t(csr_cap))) != hipSuccess) return e;
-    if ((e = send_rows.alloc(R * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
+    if ((e = send_rows.alloc(R * size_t(pair_cap) * wire)) != hipSuccess) return e;
     if ((e = recv_rows.alloc(R * size_t(pair_cap) * size_t(row_words))) != hipSuccess) return e;
+    // RCCL receives into a wire-format region when rows are packed (raw rows land in place)
+    if (rccl && packed && (e = recv_wire.alloc(R * size_t(pair_cap) * wire)) != hipSuccess) return e;
     if ((e = send_rec.alloc(R * size_t(msg_cap))) != hipSuccess) return e;
     if ((e = recv_rec.alloc(R * size_t(msg_cap))) != hipSuccess) return e;
-    return hipMemsetAsync(recv_msgs.p, 0, G * 4, st);
+    if ((e = hipMemsetAsync(recv_msgs.p, 0, G * 4, st)) != hipSuccess) return e;
+    return hipMemsetAsync(recv_pairs.p, 0, G * 4, st);
 }
 
 void RowxBufs::release() {
-    for (auto *b : {&cnt, &cnt_all, &recv_msgs, &pair_row, &csr_slot}) b->release();
+    for (auto *b : {&cnt, &cnt_all, &recv_msgs, &recv_pairs, &pair_row, &csr_slot, &bounds}) b->release();
     send_rows.release();
     recv_rows.release();
+    recv_wire.release();
     send_rec.release();
     recv_rec.release();
 }
 
+hipError_t RowxState::init(int32_t g, bool with_rccl) {
+    shards = g;
+    rccl = with_rccl;
+    const size_t S = size_t(rowx_cnt_stride(g));
+    hipError_t e;
+    if ((e = hipHostMalloc(reinterpret_cast<void **>(&h_cnt), size_t(kRing) * S * g * 4)) != hipSuccess) return e;
+    if ((e = hipHostMalloc(reinterpret_cast<void **>(&h_bounds), size_t(kRing) * 2 * g * g * 4)) != hipSuccess)
+        return e;
+    for (auto &v : ev)
+        if ((e = hipEventCreateWithFlags(&v, hipEventDisableTiming)) != hipSuccess) return e;
+    max_pairs.assign(size_t(g) * g, -1);
+    max_msgs.assign(size_t(g) * g, -1);
+    if (const char *tt = std::getenv("GSP_TEST_ROWX_TIGHT")) tight = std::atoi(tt) != 0;
+    return hipSuccess;
+}
+
+void RowxState::release() {
+    if (h_cnt) (void)hipHostFree(h_cnt);
+    if (h_bounds) (void)hipHostFree(h_bounds);
+    for (auto &v : ev)
+        if (v) (void)hipEventDestroy(v);
+    h_cnt = h_bounds = nullptr;
+    for (auto &v : ev) v = nullptr;
+}
+
+namespace {
+
+// The host reads the counts of exchange k (its event has fired or is waited for here): the
+// largest counts seen grow, and an in-process group's bytes are accounted from them.
+int rowx_see(RowxState &s, int64_t k, double *bytes) {
+    const int32_t G = s.shards, S = rowx_cnt_stride(G);
+    GSP_HIP(hipEventSynchronize(s.ev[k % RowxState::kRing]));
+    const int32_t *c = s.h_cnt + size_t(k % RowxState::kRing) * S * G;
+    for (int32_t g = 0; g < G; ++g)
+        for (int32_t h = 0; h < G; ++h) {
+            if (g == h) continue;
+            const int64_t p = c[size_t(g) * S + h], m = c[size_t(g) * S + G + h];
+            int64_t &mp = s.max_pairs[size_t(g) * G + h], &mm = s.max_msgs[size_t(g) * G + h];
+            mp = std::max(mp, p);
+            mm = std::max(mm, m);
+            if (!s.rccl) *bytes += double(p) * s.wire_bytes_per_row + double(m) * s.rec_bytes;
+        }
+    s.seen = k + 1;
+    return GSP_OK;
+}
+
+}  // namespace
+
+int rowx_collect(RowxState &s, double *bytes) {
+    while (s.seen < s.seq)
+        if (int rc = rowx_see(s, s.seen, bytes)) return rc;
+    return GSP_OK;
+}
+
 int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *bytes) {
     const int32_t G = job.shards, W = job.row_words, F = job.fanout, S = rowx_cnt_stride(G);
+    const int32_t PW = job.packed ? rowx_packed_words(W) : W;      // words per row on the wire
+    RowxState &st8 = *job.state;
     hipStream_t st = job.st;
+    st8.wire_bytes_per_row = double(PW) * 8.0;
     for (RowxShard &sh : local) {
         GSP_HIP(hipMemsetAsync(sh.x->cnt.p, 0, size_t(2 * G) * 4, st));
         GSP_HIP(hipMemcpyAsync(sh.x->cnt.p + 2 * G, sh.err, 4, hipMemcpyDeviceToDevice, st));
@@ -59,6 +129,7 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
         a.pair_cap = job.pair_cap;
         a.msg_cap = job.msg_cap;
         a.row_words = W;
+        a.packed = job.packed ? 1 : 0;
         a.out_dst = sh.out_dst;
         a.table = sh.table;
         a.pair_cnt = sh.x->cnt.p;
@@ -69,7 +140,8 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
         GSP_HIP(launch_rowx_pack(a, st));
         GSP_HIP(launch_rowx_gather(a, st));
     }
-    // counts of every shard -> cnt_all[G][2G + 1] of the first local shard, read by the host
+    // counts of every shard -> cnt_all[G][2G + 1] of the first local shard (every local shard
+    // reads that one), then to pinned memory for the sizes of later exchanges
     RowxBufs &x0 = *local[0].x;
     if (job.comm) {
         GSP_NCCL(ncclAllGather(x0.cnt.p, x0.cnt_all.p, size_t(S), ncclInt32, job.comm, st));
@@ -78,72 +150,76 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
             GSP_HIP(hipMemcpyAsync(x0.cnt_all.p + size_t(src.g) * S, src.x->cnt.p, size_t(S) * 4,
                                    hipMemcpyDeviceToDevice, st));
     }
-    GSP_HIP(hipMemcpyAsync(job.h_cnt, x0.cnt_all.p, size_t(S) * G * 4, hipMemcpyDeviceToHost, st));
-    GSP_HIP(hipStreamSynchronize(st));
-    auto pairs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * S + h]); };
-    auto msgs = [&](int32_t g, int32_t h) { return int64_t(job.h_cnt[size_t(g) * S + G + h]); };
-    for (int32_t g = 0; g < G; ++g)       // the same all-gathered flags on every rank
-        GSP_REQUIRE(job.h_cnt[size_t(g) * S + 2 * G] == 0, GSP_ERR_CAPACITY,
-                    "a receiver of shard %d got more messages than the kernel's segment bound at "
-                    "tick %d; ticks after it did not run", g, job.h_cnt[size_t(g) * S + 2 * G]);
-    for (int32_t g = 0; g < G; ++g)
-        for (int32_t h = 0; h < G; ++h)
-            GSP_REQUIRE(pairs(g, h) <= job.pair_cap && msgs(g, h) <= job.msg_cap, GSP_ERR_CAPACITY,
-                        "row exchange: shard %d sends %lld rows / %lld records to shard %d "
-                        "(capacity %lld / %lld)", g, (long long)pairs(g, h), (long long)msgs(g, h),
-                        h, (long long)job.pair_cap, (long long)job.msg_cap);
-    const size_t row_bytes = size_t(W) * 8, rec_bytes = sizeof(RowxRec);
-    double sent = 0;
+    const int64_t k = st8.seq++;
+    const int slot = int(k % RowxState::kRing);
+    GSP_HIP(hipMemcpyAsync(st8.h_cnt + size_t(slot) * S * G, x0.cnt_all.p, size_t(S) * G * 4,
+                           hipMemcpyDeviceToHost, st));
+    GSP_HIP(hipEventRecord(st8.ev[slot], st));
+    // the host reads the previous exchange's counts (its only wait: one tick behind)
+    if (k >= 1)
+        while (st8.seen < k)
+            if (int rc = rowx_see(st8, st8.seen, bytes)) return rc;
+    const int32_t *d_bounds = nullptr;
+    const size_t GG = size_t(G) * G;
+    if (job.comm || st8.tight) {
+        // sizes posted to RCCL, the same on every rank: derived from the all-gathered counts
+        // of exchanges 0 .. k - 1 (the capacity for the first exchange)
+        int32_t *hb = st8.h_bounds + size_t(slot) * 2 * GG;
+        const int64_t mpa = st8.tight ? 0 : 256, mma = st8.tight ? 0 : 1024;
+        const int64_t div = st8.tight ? int64_t(1) << 40 : 16;
+        for (size_t i = 0; i < GG; ++i) {
+            const int64_t mp = st8.max_pairs[i], mm = st8.max_msgs[i];
+            hb[i] = int32_t(mp < 0 ? job.pair_cap : std::min<int64_t>(job.pair_cap, mp + mp / div + mpa));
+            hb[GG + i] = int32_t(mm < 0 ? job.msg_cap : std::min<int64_t>(job.msg_cap, mm + mm / div + mma));
+        }
+        int32_t *db = x0.bounds.p + size_t(slot) * 2 * GG;
+        GSP_HIP(hipMemcpyAsync(db, hb, 2 * GG * 4, hipMemcpyHostToDevice, st));
+        d_bounds = db;
+    }
+    for (RowxShard &sh : local)
+        GSP_HIP(launch_rowx_check(x0.cnt_all.p, d_bounds, G, sh.g, job.pair_cap, job.msg_cap, job.tick,
+                                  sh.err, sh.x->recv_pairs.p, sh.x->recv_msgs.p, st));
     if (job.comm) {
+        const int32_t *hb = st8.h_bounds + size_t(slot) * 2 * GG;
         RowxShard &sh = local[0];
         const int32_t me = sh.g;
+        double sent = 0;
         GSP_NCCL(ncclGroupStart());
         for (int32_t h = 0; h < G; ++h) {
             if (h == me) continue;
             const size_t reg = size_t(rowx_region(h, me));      // same index for h's region here
             const size_t so = reg * size_t(job.pair_cap), mo = reg * size_t(job.msg_cap);
-            // full-view rows are 512 KB at 262,144 nodes: a region can pass 2^31 elements, so
-            // rows move in pieces of at most kPiece words (matched in order on both sides)
-            const size_t ns = size_t(pairs(me, h)) * W, nr = size_t(pairs(h, me)) * W;
+            const size_t bs_p = size_t(hb[size_t(me) * G + h]), bs_m = size_t(hb[GG + size_t(me) * G + h]);
+            const size_t br_p = size_t(hb[size_t(h) * G + me]), br_m = size_t(hb[GG + size_t(h) * G + me]);
+            uint64_t *rbase = job.packed ? sh.x->recv_wire.p : sh.x->recv_rows.p;
+            // rows move in pieces of at most kPiece words (a full-view region can pass 2^31
+            // elements), matched in order on both sides
+            const size_t ns = bs_p * PW, nr = br_p * PW;
             for (size_t o = 0; o < ns; o += kPiece)
-                GSP_NCCL(ncclSend(sh.x->send_rows.p + so * W + o, std::min(kPiece, ns - o), ncclUint64,
+                GSP_NCCL(ncclSend(sh.x->send_rows.p + so * PW + o, std::min(kPiece, ns - o), ncclUint64,
                                   h, job.comm, st));
-            if (msgs(me, h))
-                GSP_NCCL(ncclSend(sh.x->send_rec.p + mo, size_t(msgs(me, h)) * 3, ncclInt32, h,
-                                  job.comm, st));
+            if (bs_m)
+                GSP_NCCL(ncclSend(sh.x->send_rec.p + mo, bs_m * 3, ncclInt32, h, job.comm, st));
             for (size_t o = 0; o < nr; o += kPiece)
-                GSP_NCCL(ncclRecv(sh.x->recv_rows.p + so * W + o, std::min(kPiece, nr - o), ncclUint64,
-                                  h, job.comm, st));
-            if (msgs(h, me))
-                GSP_NCCL(ncclRecv(sh.x->recv_rec.p + mo, size_t(msgs(h, me)) * 3, ncclInt32, h,
-                                  job.comm, st));
-            sent += double(pairs(me, h)) * row_bytes + double(msgs(me, h)) * rec_bytes;
+                GSP_NCCL(ncclRecv(rbase + so * PW + o, std::min(kPiece, nr - o), ncclUint64, h, job.comm, st));
+            if (br_m)
+                GSP_NCCL(ncclRecv(sh.x->recv_rec.p + mo, br_m * 3, ncclInt32, h, job.comm, st));
+            sent += double(bs_p) * double(PW) * 8.0 + double(bs_m) * 12.0;
         }
         GSP_NCCL(ncclGroupEnd());
+        *bytes += sent;
+        if (job.packed)
+            GSP_HIP(launch_rowx_unpack(sh.x->recv_wire.p, sh.x->recv_rows.p, sh.x->recv_pairs.p, G, me,
+                                       job.pair_cap, W, 1, st));
     } else {
         for (RowxShard &src : local)
-            for (RowxShard &dst : local) {
-                const int32_t g = src.g, h = dst.g;
-                if (g == h) continue;
-                // src's region for h (send side), dst's region for g (receive side)
-                const size_t sr = size_t(rowx_region(h, g)), rr = size_t(rowx_region(g, h));
-                const size_t so = sr * size_t(job.pair_cap), mo = sr * size_t(job.msg_cap);
-                const size_t ro = rr * size_t(job.pair_cap), qo = rr * size_t(job.msg_cap);
-                if (pairs(g, h))
-                    GSP_HIP(hipMemcpyAsync(dst.x->recv_rows.p + ro * W, src.x->send_rows.p + so * W,
-                                           size_t(pairs(g, h)) * row_bytes, hipMemcpyDeviceToDevice, st));
-                if (msgs(g, h))
-                    GSP_HIP(hipMemcpyAsync(dst.x->recv_rec.p + qo, src.x->send_rec.p + mo,
-                                           size_t(msgs(g, h)) * rec_bytes, hipMemcpyDeviceToDevice, st));
-                sent += double(pairs(g, h)) * row_bytes + double(msgs(g, h)) * rec_bytes;
-            }
+            for (RowxShard &dst : local)
+                if (src.g != dst.g)
+                    GSP_HIP(launch_rowx_local_copy(src.x->send_rows.p, src.x->send_rec.p, dst.x->recv_rows.p,
+                                                   dst.x->recv_rec.p, x0.cnt_all.p, G, src.g, dst.g,
+                                                   job.pair_cap, job.msg_cap, W, job.packed ? 1 : 0, st));
     }
-    *bytes += sent;
-    for (size_t i = 0; i < local.size(); ++i) {
-        RowxShard &sh = local[i];
-        int32_t *hr = job.h_recv + i * size_t(G);
-        for (int32_t h = 0; h < G; ++h) hr[h] = h == sh.g ? 0 : int32_t(msgs(h, sh.g));
-        GSP_HIP(hipMemcpyAsync(sh.x->recv_msgs.p, hr, size_t(G) * 4, hipMemcpyHostToDevice, st));
+    for (RowxShard &sh : local) {
         GSP_HIP(launch_rowx_recv_deg(sh.x->recv_rec.p, sh.x->recv_msgs.p, G, sh.g, job.msg_cap,
                                      sh.row0, sh.deg, st));
         GSP_HIP(launch_exclusive_scan(sh.deg + sh.row0, sh.off, sh.rows, sh.tile_sum, st));

@@ -12,11 +12,18 @@
 //   csr      receiver CSR over the local rows: local messages (csr_slot = local row) and
 //            received records (csr_slot = -(region * pair_cap + pair) - 1 into the remote rows).
 // HBM layout per shard, one REGION per other shard (rowx_region; none for the shard itself):
-// send_rows[G-1][pair_cap][row_words], send_rec[G-1][msg_cap], recv_rows[G-1][pair_cap]
-// [row_words], recv_rec[G-1][msg_cap].  pair_cap = max rows of a shard
+// send_rows[G-1][pair_cap][wire_words], send_rec[G-1][msg_cap], recv_rows[G-1][pair_cap]
+// [row_words] (what the tick kernels read), recv_wire[G-1][pair_cap][wire_words] (RCCL
+// receives, packed rows only), recv_rec[G-1][msg_cap].  pair_cap = max rows of a shard
 // makes every tick fit (a sender row goes to a shard at most once); an engine may size it
 // smaller for large rows, in which case a count above the capacity fails the tick
-// (GSP_ERR_CAPACITY) and nothing is written out of bounds.
+// (GSP_ERR_CAPACITY, set on the device) and nothing is written out of bounds.
+//
+// Wire format.  A full-view row (u16 entries) travels as it is.  A partial-view row (V u64
+// entries id << 32 | hb << 5 | ts5, sorted by id, empty slots last) travels PACKED: the low 16
+// bits of each id (u16[V]), each value (u16[V]) and, because the ids ascend, their high 5 bits
+// as 33 run boundaries: bound[h] = entries whose id >> 16 is below h (bound[32] = the entry
+// count) -- 4 V + 66 bytes instead of 8 V (1,090 B instead of 2,048 B at V = 256).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -29,11 +36,15 @@ struct RowxRec {
     int32_t pair;    // index of the sender's row in the (src shard -> dst shard) region
 };
 
+// 8-byte words of a packed partial-view row of V entries
+__host__ __device__ inline int32_t rowx_packed_words(int32_t V) { return (4 * V + 66 + 7) / 8; }
+
 struct RowxArgs {
     int32_t n, shards, shard, fanout;
     int32_t row0, rows;              // this shard's rows
     int64_t pair_cap, msg_cap;       // per (src shard, dst shard) region
-    int32_t row_words;               // 8-byte words per row
+    int32_t row_words;               // 8-byte words per row (packed: V, the entries per row)
+    int32_t packed;                  // 1: send_rows holds packed rows (rowx_packed_words(V) each)
     const int32_t *out_dst;          // [rows * fanout] global destination ids, -1 = none
     const uint64_t *table;           // this shard's rows of the tick the messages were sent in
     int32_t *pair_cnt;               // [G] pairs per destination shard (zeroed before pack)
@@ -58,6 +69,29 @@ __host__ __device__ inline int64_t rowx_region(int32_t h, int32_t self) {
 
 hipError_t launch_rowx_pack(const RowxArgs &a, hipStream_t st);
 hipError_t launch_rowx_gather(const RowxArgs &a, hipStream_t st);
+
+// After the counts all-gather (cnt_all[G][2G + 1]: pairs per destination, records per
+// destination, capacity flag, of every shard): shard `self` checks every count against its
+// capacity and -- RCCL path -- against the sizes the host posted for this exchange (bounds
+// [2][G][G]: pairs, records; null: the capacities only), and any shard's capacity flag; the
+// first failure sets *err = tick | kRowxErrBit (tick if a shard's receipt flag).  It writes the
+// true counts this shard receives, clamped to what arrived, to recv_pairs[G] / recv_msgs[G]:
+// the in-band counts every later kernel of the exchange reads.
+constexpr int32_t kRowxErrBit = 1 << 24;
+hipError_t launch_rowx_check(const int32_t *cnt_all, const int32_t *bounds, int32_t shards, int32_t self,
+                             int64_t pair_cap, int64_t msg_cap, int32_t tick, int32_t *err,
+                             int32_t *recv_pairs, int32_t *recv_msgs, hipStream_t st);
+// Received rows of every source shard h != self (recv_pairs[h] of them) into recv_rows:
+// packed rows decoded from recv_wire, raw rows copied from it.
+hipError_t launch_rowx_unpack(const uint64_t *recv_wire, uint64_t *recv_rows, const int32_t *recv_pairs,
+                              int32_t shards, int32_t self, int64_t pair_cap, int32_t row_words,
+                              int32_t packed, hipStream_t st);
+// In-process groups: shard g's send region for h -> shard h's receive region for g, rows
+// (decoded when packed) and records, sized by the device counts (cnt_all row g).
+hipError_t launch_rowx_local_copy(const uint64_t *send_rows, const RowxRec *send_rec, uint64_t *recv_rows,
+                                  RowxRec *recv_rec, const int32_t *cnt_all, int32_t shards, int32_t g,
+                                  int32_t h, int64_t pair_cap, int64_t msg_cap, int32_t row_words,
+                                  int32_t packed, hipStream_t st);
 // deg[row0 + rec.dst]++ for the received records of every source shard h != self
 // (counts: recv_msgs[h])
 hipError_t launch_rowx_recv_deg(const RowxRec *recv_rec, const int32_t *recv_msgs, int32_t shards,

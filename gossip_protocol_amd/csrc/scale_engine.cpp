@@ -72,7 +72,7 @@ struct gsp_scale {
                                // column tiles of one GPU's job (DESIGN.md "Column tiles")
     bool rowmode = false;      // row layout (G > 1): sender rows move between shards
     int64_t pair_cap = 0, msg_cap = 0;
-    int32_t *h_cnt = nullptr, *h_recv = nullptr;   // pinned exchange counts (row layout)
+    gsp::RowxState rowx;       // row layout: the exchange's count ring and posted sizes
     int32_t *h_err = nullptr;  // pinned mirror of the shards' capacity flags, refreshed by an
                                // async copy at the end of every gsp_scale_step call
     int32_t max_segment = INT32_MAX;     // segments past kMaxSegment take the HBM sort
@@ -269,8 +269,8 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
         GSP_HIP(sh.bitmap.alloc(size_t(n) * size_t(s->stride / 8) * (s->shared ? s->local.size() : 1)));
     }
     if (s->rowmode)
-        GSP_HIP(sh.x.alloc(s->shards, s->pair_cap, s->msg_cap, int32_t(s->stride / 4),
-                           int64_t(n) * s->p.fanout, st));
+        GSP_HIP(sh.x.alloc(s->shards, s->pair_cap, s->msg_cap, int32_t(s->stride / 4), false,
+                           s->comm != nullptr, int64_t(n) * s->p.fanout, st));
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kDigSlots * gsp::kDigFields;
     GSP_HIP(sh.dig.alloc(dig));
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * sizeof(unsigned long long), st));
@@ -396,8 +396,8 @@ int exchange_row_counts(gsp_scale *s, int32_t t) {
 // Row layout: the sender rows of tick t_sent's cross-shard messages move to their receivers'
 // shards (rowx_host.cpp); every shard gets the receiver CSR of tick t_sent + 1.
 int exchange_rows(gsp_scale *s, int32_t t_sent) {
-    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, int32_t(s->stride / 4), s->pair_cap,
-                     s->msg_cap, s->comm, s->st, s->h_cnt, s->h_recv};
+    gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, int32_t(s->stride / 4), false, s->pair_cap,
+                     s->msg_cap, s->comm, s->st, t_sent + 1, &s->rowx};
     std::vector<gsp::RowxShard> v;
     for (Shard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p,
@@ -417,9 +417,15 @@ int exchange_rows(gsp_scale *s, int32_t t_sent) {
 // (GSP_TEST_MAX_SEGMENT) no segment overflows: segments past kMaxSegment are sorted in HBM.
 int mirrored_err(gsp_scale *s) {
     for (size_t i = 0; i < s->local.size(); ++i)
-        GSP_REQUIRE(s->h_err[i] == 0, GSP_ERR_CAPACITY,
+    {
+        const int32_t e = s->h_err[i];
+        GSP_REQUIRE(!(e & gsp::kRowxErrBit), GSP_ERR_CAPACITY,
+                    "row exchange at tick %d: a shard's rows or records passed the region capacity "
+                    "or the size posted to RCCL; ticks after it did not run", e & ~gsp::kRowxErrBit);
+        GSP_REQUIRE(e == 0, GSP_ERR_CAPACITY,
                     "a receiver got more than %d messages at tick %d; ticks after it did not run",
-                    s->max_segment, s->h_err[i]);
+                    s->max_segment, e);
+    }
     return GSP_OK;
 }
 
@@ -502,6 +508,8 @@ int collect_timing(gsp_scale *s) {
         s->free_events.push_back(t.c);
     }
     s->pending.clear();
+    if (s->rowmode)
+        if (int rc = gsp::rowx_collect(s->rowx, &s->perf.xgmi_bytes)) return rc;
     return GSP_OK;
 }
 
@@ -593,9 +601,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_err), size_t(local_shards) * 4));
     std::memset(s->h_err, 0, size_t(local_shards) * 4);
     if (s->rowmode) {
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_cnt),
-                              size_t(gsp::rowx_cnt_stride(shards)) * shards * 4));
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_recv), size_t(local_shards) * shards * 4));
+        GSP_HIP(s->rowx.init(shards, nccl_id != nullptr));
     }
     if (nccl_id) {
         ncclUniqueId id;
@@ -682,8 +688,7 @@ int gsp_scale_destroy(gsp_scale *s) {
     for (Shard &sh : s->local) sh.release();
     s->long_tpl.release();
     if (s->comm) (void)ncclCommDestroy(s->comm);
-    if (s->h_cnt) (void)hipHostFree(s->h_cnt);
-    if (s->h_recv) (void)hipHostFree(s->h_recv);
+    s->rowx.release();
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
