@@ -81,16 +81,9 @@ struct gsp_pview {
     bool pos_scatter = false;    // one shard, no join schedule: the receiver CSR is scattered from
                                  // the positions the send kernel's deg atomics returned (the
                                  // JOINREP append and the row exchange keep the fill counters)
-    bool split_sync = false;     // GSP_PV_SPLITSYNC=1: exact split grids from the counts read
-                                 // back, one stream sync per tick; default: persistent grids, no
-                                 // host wait (gsp_pview_step queues its ticks back to back)
-    int32_t cus = 0;             // compute units (overflow kernel grid)
-    int32_t grid_margin = 100;   // GSP_PV_GRID_MARGIN: predicted split grids, percent over the
-                                 // last bucket sizes seen
-    int32_t test_grid_cap = 0;   // GSP_TEST_PV_GRID_CAP (tests: force the overflow kernel)
-    int32_t *h_kcount = nullptr; // pinned [8] for split_sync
-    int32_t *h_kseen = nullptr;  // pinned [local][8]: each shard's bucket sizes, copied back
-                                 // asynchronously every tick (they size the next tick's grids)
+    int32_t cus = 0;             // compute units (drain grid)
+    int32_t *h_kcount = nullptr; // pinned [8]: the bucket sizes, the split kernels' grids
+    hipEvent_t kcount_ev = nullptr;
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
@@ -160,10 +153,7 @@ struct gsp_pview {
         a.prof = sh.prof.p;
         a.split = split;
         a.kcount_host = h_kcount;
-        a.kcount_seen = h_kseen ? h_kseen + 8 * (&sh - local.data()) : nullptr;
-        a.cus = cus;
-        a.grid_margin = grid_margin;
-        a.test_grid_cap = test_grid_cap;
+        a.kcount_event = kcount_ev;
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
@@ -432,17 +422,12 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
     if (const char *sp = std::getenv("GSP_PV_SPLIT")) s->split = std::atoi(sp);
-    if (const char *ss = std::getenv("GSP_PV_SPLITSYNC")) s->split_sync = std::atoi(ss) != 0;
     if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
-    if (const char *gc = std::getenv("GSP_TEST_PV_GRID_CAP")) s->test_grid_cap = std::max(0, std::atoi(gc));
-    if (const char *gm = std::getenv("GSP_PV_GRID_MARGIN")) s->grid_margin = std::max(0, std::min(1000, std::atoi(gm)));
-    if (s->split_sync && s->split && s->sort_rows)
+    if (s->split && s->sort_rows) {
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
-    GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
-    if (!s->split_sync && s->split && s->sort_rows) {
-        GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kseen), size_t(local_shards) * 8 * 4));
-        std::memset(s->h_kseen, 0xFF, size_t(local_shards) * 8 * 4);    // -1: nothing seen yet
+        GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
     }
+    GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
@@ -563,7 +548,7 @@ int gsp_pview_destroy(gsp_pview *s) {
     s->rowx.release();
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->h_kcount) (void)hipHostFree(s->h_kcount);
-    if (s->h_kseen) (void)hipHostFree(s->h_kseen);
+    if (s->kcount_ev) (void)hipEventDestroy(s->kcount_ev);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;
@@ -607,9 +592,6 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
             if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 4, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
-            if (s->h_kseen)          // never waited on: the next ticks' grid predictions
-                GSP_HIP(hipMemcpyAsync(s->h_kseen + 8 * (&sh - s->local.data()), sh.kcount.p, 8 * 4,
-                                       hipMemcpyDeviceToHost, s->st));
         }
         // ranks: the receipt kernels' capacity flags, MAX over the ranks before any tick kernel
         // of t reads them -- every rank's rows of t run, or none does, and every rank's flag

@@ -8,9 +8,9 @@
 //   merges, heavy rows first): k = 6, 7 as 256-lane rows in 20 KB of LDS, k = 5 / k = 4 as
 //   128-lane rows merged in place (one key buffer, 11.3 / 9.8 KB, PvSharedIP), k <= 3 as
 //   128-lane rows in 10 KB; k = 0 rows of the plain protocol skip steps 2-5 (pv_own_only).
-//   The grids are predicted on the host from an earlier tick's bucket sizes (no host wait);
-//   pview_tick_overflow_kernel runs the rows past a grid.  pview_tick_kernel is the one-kernel
-//   form (GSP_PV_SPLIT=0: one 256-lane workgroup per row, any k).  The row body:
+//   Each range's grid is its bucket size, read back behind an event after the receipt kernel.
+//   pview_tick_kernel is the one-kernel form (GSP_PV_SPLIT=0: one 256-lane workgroup per row,
+//   any k).  The row body:
 //   1. loads: the own view is requested first; the receipt record is read by every wave
 //      (no barrier) and the k sender views follow, one coalesced 2 KB row each;
 //   2. keys: each view is a sorted block of 256 slots of 32-bit keys id << 11 | source << 8
@@ -56,11 +56,11 @@ constexpr uint32_t kKeyMax = 0xFFFFFFFFu;             // id field 2^21 - 1: abov
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
 static_assert(kMaxBlocks == 8, "the merge tree assumes 8 blocks of 256 keys");
 
-// threadIdx.x as a value the compiler cannot see through: the persistent split kernels loop
-// over rows, and every lane-position value derived from the thread index (slot offsets, LDS
-// addresses) would otherwise be hoisted out of that loop and kept live across the row body,
-// spilling it; an opaque copy per use keeps them per-row temporaries.
-// (Its range [0, NT) is restated, so loops over a lane's slots still unroll.)
+// threadIdx.x as a value the compiler cannot see through: an opaque copy per use keeps the
+// lane-position values derived from it (slot offsets, LDS addresses) short-lived temporaries
+// instead of registers held across the row body (round 4: the looping overflow kernel spilled
+// without it; kept since, as the measured code).  Its range [0, NT) is restated, so loops
+// over a lane's slots still unroll.
 template <int NT>
 __device__ __forceinline__ int32_t pv_tid() {
     int32_t t = int32_t(threadIdx.x);
@@ -1021,63 +1021,16 @@ __global__ void __launch_bounds__(kPvBlock, 8) pview_tick_kernel(PviewTickArgs a
 // Split form (rows bucketed by k, a.order set): the rows that merge at most 3 messages
 // (kQhi = 3: at most 4 sources, 1024 keys) run as 128-lane rows in 10 KB of LDS -- 16 rows
 // per CU instead of 8, two waves per row instead of four, each lane holding two slots of
-// every source -- k = 4 and k = 5 as 128-lane rows in 12.5 / 15 KB, k = 6, 7 as 256-lane
-// rows in 20 KB.  Workgroup b runs the b-th row of its buckets' k-descending order; rows at
-// or past the grid belong to pview_tick_overflow_kernel (the grid is either the exact bucket
-// size, read back by the host, or the host's prediction from the last counts it has seen).
+// every source -- k = 4 and k = 5 as 128-lane rows merged in place in 9.8 / 11.3 KB, k = 6, 7
+// as 256-lane rows in 20 KB.  One kernel per k range, heavy rows first; workgroup b runs the
+// b-th row of the range's k-descending order, the grid is the range's bucket size (read back
+// by the host after the receipt kernel: launch_pview_tick).
 template <int kExt, int NT, int kQlo, int kQhi, int kMinWaves = 8, bool kIP = false>
 __global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTickArgs a) {
     constexpr int kKeys = NT == 64 ? 512 : kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots;
     __shared__ std::conditional_t<kIP, PvSharedIP<kKeys>, PvShared<kKeys>> sh;
     static_assert(NT != 64 || kQhi <= 1, "one-wave rows hold at most 2 sources");
-    int32_t total = 0;
-#pragma unroll
-    for (int q = kQlo; q <= kQhi; ++q) total += a.kcount[q];
-    const int32_t b = int32_t(blockIdx.x);
-    if (b >= total) return;
-    pv_row<kExt, NT, kQlo, kQhi>(a, sh, pv_row_of<kQlo, kQhi>(a, b));
-}
-
-// The split kernels' k ranges, in launch order (launch_pview_tick).
-constexpr int kPvRanges = 4;
-__device__ __forceinline__ int32_t pv_range_lo(int32_t j) { return j == 0 ? 6 : j == 1 ? 5 : j == 2 ? 4 : 0; }
-__device__ __forceinline__ int32_t pv_range_hi(int32_t j) { return j == 0 ? 7 : j == 1 ? 5 : j == 2 ? 4 : 3; }
-
-// The rows of every split range at or past that kernel's grid (a.split_grid[j]): the grids the
-// host predicted were too small for this tick's buckets.  A fixed grid; each workgroup runs
-// such rows b, b + grid, ... as 256-lane rows (any k) until none is left -- usually none, and
-// the kernel costs one short launch.  This is what lets the host launch a tick without
-// reading its bucket sizes back: gsp_pview_step queues ticks with no host wait.
-template <int kExt>
-__global__ void __launch_bounds__(kPvBlock, 8) pview_tick_overflow_kernel(PviewTickArgs a) {
-    __shared__ PvShared<kMaxKeys> sh;
-    int32_t over[kPvRanges], total = 0;
-#pragma unroll
-    for (int j = 0; j < kPvRanges; ++j) {
-        int32_t c = 0;
-        for (int32_t q = pv_range_lo(j); q <= pv_range_hi(j); ++q) c += a.kcount[q];
-        over[j] = c > a.split_grid[j] ? c - a.split_grid[j] : 0;
-        total += over[j];
-    }
-    for (int32_t b = int32_t(blockIdx.x); b < total; b += int32_t(gridDim.x)) {
-        int32_t j = 0, off = b;                  // block-uniform: the range and the offset
-#pragma unroll
-        for (int q = 0; q < kPvRanges - 1; ++q)
-            if (j == q && off >= over[q]) { off -= over[q]; j = q + 1; }
-        int32_t pos = a.split_grid[j] + off;     // the position in the range's k-descending order
-        int32_t q = pv_range_hi(j);
-        for (; q > pv_range_lo(j); --q) {
-            const int32_t c = a.kcount[q];
-            if (pos < c) break;
-            pos -= c;
-        }
-        // the scalars every row derives its constants from, opaque per row (as pv_tid): hoisted
-        // out of this loop they would stay live across the row body
-        PviewTickArgs ai = a;
-        asm volatile("" : "+s"(ai.tick), "+s"(ai.h0), "+s"(ai.tremove), "+s"(ai.view));
-        pv_row<kExt, kPvBlock, 0, 7>(ai, sh, ai.order[int64_t(q) * ai.rows + pos]);
-        __syncthreads();                         // the row's LDS is read by its view write
-    }
+    pv_row<kExt, NT, kQlo, kQhi>(a, sh, pv_row_of<kQlo, kQhi>(a, int32_t(blockIdx.x)));
 }
 
 // The K smallest senders of every receiver's CSR segment, ascending (the canonical receipt
@@ -1412,58 +1365,32 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
                     (a.ev.buf != nullptr ? kExtEv : 0) | (a.evict_rot ? kExtRot : 0);
     if (a.order && a.split) {
         // split form: k = 6, 7 / k = 5 / k = 4 / k <= 3 (pview_tick_split_kernel), in this order
-        // (the heavy rows first).  Grids: the exact bucket sizes, read back synchronously
-        // (a.kcount_host, GSP_PV_SPLITSYNC=1), or -- by default, no host wait -- predicted from
-        // the last counts the host has seen (a.kcount_seen, copied back asynchronously each
-        // tick), with a.grid_margin % + 1024 rows of margin: a host that queues many ticks
-        // predicts all of them from one tick's counts while the buckets drift (config 5, ticks
-        // 6-25 from tick 5: the k = 6, 7 bucket grows by a third as in-degrees skew); a
-        // workgroup past its bucket exits after reading the counts.  Every row past a grid is
-        // run by the overflow kernel.
+        // (the heavy rows first), each on a grid of exactly its bucket's rows: the bucket sizes
+        // are copied back behind an event after the receipt kernel and the host waits for it
+        // (round 5: on one box, ticks 6-25, 5.36 ms against 5.42 for round 3's grids predicted
+        // without a wait plus an overflow kernel, and 6.7-13 ms for persistent kernels pulling
+        // row chunks from per-XCD heads -- DESIGN.md 4b)
+        if (!a.kcount_host || !a.kcount_event) return hipErrorInvalidValue;
         PviewTickArgs b = a;
         int32_t c[8];
-        const bool exact = a.kcount_host != nullptr;
-        if (exact) {
-            if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-                hipStreamSynchronize(st) != hipSuccess)
-                return hipGetLastError();
-            for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
-        } else {
-            for (int q = 0; q < 8; ++q) c[q] = a.kcount_seen ? a.kcount_seen[q] : -1;
-        }
-        auto grid = [&](int lo, int hi) {
-            int64_t g = 0;
-            for (int q = lo; q <= hi; ++q) {
-                if (c[q] < 0 || c[q] > a.rows) {                   // nothing seen yet: every row
-                    g = a.rows;
-                    break;
-                }
-                g += c[q];
-            }
-            if (!exact) g += g * a.grid_margin / 100 + 1024;
-            if (!exact && a.test_grid_cap > 0 && g > a.test_grid_cap) g = a.test_grid_cap;
-            return int32_t(g < a.rows ? g : a.rows);
-        };
-        b.split_grid[0] = grid(6, 7);
-        b.split_grid[1] = grid(5, 5);
-        b.split_grid[2] = grid(4, 4);
-        b.split_grid[3] = grid(0, 3);
-        const int32_t cus = a.cus > 0 ? a.cus : 256;
-        const unsigned gov = unsigned(std::min<int64_t>(int64_t(cus) * 8, a.rows));
-        // k = 6, 7: 256-lane rows in 20 KB, 8 waves per SIMD; k = 5 / k = 4: 128-lane rows merged in
-        // place (PvSharedIP, 11.3 / 9.8 KB) at 6 / 7 waves per SIMD (8 / 7 spill 24 / 20 B);
-        // k <= 3: 128-lane rows in 10 KB.  DESIGN.md 4b records the A/Bs behind each choice.
-#define GSP_PV_K67(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 256, 6, 7, 8>), dim3(b.split_grid[0]), dim3(256), 0, st, b);
-#define GSP_PV_K5(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 5, 5, 6, true>), dim3(b.split_grid[1]), dim3(128), 0, st, b);
-#define GSP_PV_K4(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 4, 4, 7, true>), dim3(b.split_grid[2]), dim3(128), 0, st, b);
-#define GSP_PV_K03(E) hipLaunchKernelGGL((pview_tick_split_kernel<E, 128, 0, 3>), dim3(b.split_grid[3]), dim3(128), 0, st, b);
+        if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipEventRecord(a.kcount_event, st) != hipSuccess || hipEventSynchronize(a.kcount_event) != hipSuccess)
+            return hipGetLastError();
+        for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
+        const unsigned g67 = unsigned(c[6] + c[7]), g5 = unsigned(c[5]), g4 = unsigned(c[4]),
+                       g03 = unsigned(c[0] + c[1] + c[2] + c[3]);
+        // k = 6, 7: 256-lane rows in 20 KB, 8 waves per SIMD (8 rows per CU); k = 5 / k = 4:
+        // 128-lane rows merged in place (PvSharedIP, 11.3 / 9.8 KB) at 6 / 7 waves per SIMD (12 /
+        // 14 rows; 8 / 7 spill 24 / 20 B); k <= 3: 128-lane rows in 10 KB (16 rows per CU).
+        // DESIGN.md 4b records the A/Bs behind each choice.
+#define GSP_PV_RANGE(E, NT, LO, HI, W, IP, G) \
+        if (G) hipLaunchKernelGGL((pview_tick_split_kernel<E, NT, LO, HI, W, IP>), dim3(G), dim3(NT), 0, st, b);
 #define GSP_PV_SPLIT_LAUNCH(E)                                                                            \
     do {                                                                                                  \
-        if (b.split_grid[0]) GSP_PV_K67(E)                                                                \
-        if (b.split_grid[1]) GSP_PV_K5(E)                                                                 \
-        if (b.split_grid[2]) GSP_PV_K4(E)                                                                 \
-        if (b.split_grid[3]) GSP_PV_K03(E)                                                                \
-        if (!exact) hipLaunchKernelGGL((pview_tick_overflow_kernel<E>), dim3(gov), dim3(kPvBlock), 0, st, b); \
+        GSP_PV_RANGE(E, 256, 6, 7, 8, false, g67)                                                       \
+        GSP_PV_RANGE(E, 128, 5, 5, 6, true, g5)                                                         \
+        GSP_PV_RANGE(E, 128, 4, 4, 7, true, g4)                                                         \
+        GSP_PV_RANGE(E, 128, 0, 3, 8, false, g03)                                                       \
     } while (0)
         switch (ext) {      // evict_order 1: the plain protocol's kernel, or the superset one
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
@@ -1474,10 +1401,7 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
             default: GSP_PV_SPLIT_LAUNCH(kExtRot | kExtPol | kExtEv); break;
         }
 #undef GSP_PV_SPLIT_LAUNCH
-#undef GSP_PV_K67
-#undef GSP_PV_K5
-#undef GSP_PV_K4
-#undef GSP_PV_K03
+#undef GSP_PV_RANGE
         if (a.drain) {
             const hipError_t e = launch_pview_drain(b, st);
             if (e != hipSuccess) return e;

@@ -63,17 +63,8 @@ struct PviewTickArgs {
                                  // of the k-descending order (one code variant per CU stretch)
     unsigned long long *prof;    // diagnostics: per-phase cycles of sampled rows (or null)
     int32_t split;               // with order set: rows bucketed by k into four kernels
-    int32_t *kcount_host;        // pinned [8]: the split kernels' grids are the exact bucket
-                                 // sizes, read back with a stream sync (GSP_PV_SPLITSYNC=1), or
-                                 // null: predicted grids + the overflow kernel, no host wait
-    const int32_t *kcount_seen;  // host, pinned [8]: the last bucket sizes copied back (any
-                                 // value is safe: it only sizes grids), or null
-    int32_t cus;                 // compute units of the device (overflow kernel grid)
-    int32_t split_grid[4];       // set by launch_pview_tick: the split kernels' grids
-    int32_t grid_margin;         // predicted grids: last counts seen * (100 + grid_margin) / 100
-                                 // + 1024 (GSP_PV_GRID_MARGIN, percent)
-    int32_t test_grid_cap;       // tests only (GSP_TEST_PV_GRID_CAP): cap on every predicted
-                                 // split grid, so the overflow kernel runs most rows (0: none)
+    int32_t *kcount_host;        // pinned [8]: the split kernels' grids, the bucket sizes read
+    hipEvent_t kcount_event;     // back behind this event after the receipt kernel
     int32_t evict_rot;           // evict_order 1: eviction ties by the rotated id (gossip.h)
     int32_t *rows_run;           // tests only (GSP_TEST_PV_COUNT_ROWS=1): [1] counter of this
                                  // tick, +1 per row a tick kernel runs (every row exactly once,

@@ -2,6 +2,7 @@
 """BASELINE config 5 (partial view) alone: the `pview` line item of bench.py.
 
     python scripts/bench_pview.py [--nodes 1048576] [--steps K] [--warmup W] [--no-cpu-baseline]
+                                  [--inbox 0]
     python -m torch.distributed.run --nproc-per-node N scripts/bench_pview.py ...   (row shards)
 """
 import argparse
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inbox", type=int, default=None, help="0: drain all (default: bench.PV_KW's 7)")
     ap.add_argument("--group", type=int, default=1,
                     help="G row shards inside this process on one GPU (exchange by device copies)")
     args = ap.parse_args()
@@ -33,7 +35,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
     out = run_pview(args.nodes, args.steps, args.warmup, world, local, dist,
-                    not args.no_cpu_baseline, group=args.group)
+                    not args.no_cpu_baseline, group=args.group, inbox=args.inbox)
     if out is not None:
         print(json.dumps(dict(out, n_gpus=world, steps=args.steps, warmup=args.warmup)), flush=True)
     if dist is not None:

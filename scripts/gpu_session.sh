@@ -21,7 +21,7 @@ step() {   # step <name> <timeout> cmd...
 for s in "$@"; do
     case $s in
         tests) step tests 1100 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
-        tests:*) step tests_k 900 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests:}" ;;
+        tests:*) step tests_k 600 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests:}" ;;
         smoke) step smoke 200 python -u -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python -u $R/bench.py ;;
         bench5) step bench5 300 python -u $R/scripts/bench_pview.py --steps 20 --warmup 5 --no-cpu-baseline ;;

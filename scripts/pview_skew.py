@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--sample", default="25,50,75,100")
     ap.add_argument("--orders", default="0,1")
     ap.add_argument("--out", default="")
+    ap.add_argument("--inbox", type=int, default=7, help="0: drain all")
     args = ap.parse_args()
     from gossip_protocol_amd import _lib
     from gossip_protocol_amd.pview import PviewEngine
@@ -38,7 +39,7 @@ def main():
     out = {"nodes": n, "ticks": args.ticks, "orders": {}}
     for order in [int(x) for x in args.orders.split(",")]:
         rows = []
-        with PviewEngine(n, view=256, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=10,
+        with PviewEngine(n, view=256, fanout=3, inbox=args.inbox, drop_pct=10, fail_mode=2, fail_tick=10,
                          fail_ppm=50000, seed=0x5EED, max_ticks=args.ticks, evict_order=order) as eng:
             done, last = 0, eng.perf()
             for s in samples:
@@ -55,7 +56,11 @@ def main():
                 k = np.minimum(d, 7)
                 mix = np.bincount(k, minlength=8) / len(k)
                 dg = eng.digest(s)
-                rows.append({"tick": s, "deg_max": int(d.max()), "deg_p99": float(np.percentile(d, 99)),
+                lg = d[d > 7]
+                rows.append({"tick": s, "long_rows": int(len(lg)), "long_msgs": int(lg.sum()),
+                             "long_k_p50": float(np.percentile(lg, 50)) if len(lg) else 0.0,
+                             "long_k_p99": float(np.percentile(lg, 99)) if len(lg) else 0.0,
+                             "deg_max": int(d.max()), "deg_p99": float(np.percentile(d, 99)),
                              "deg_p999": float(np.percentile(d, 99.9)), "k_mix": [round(x, 4) for x in mix],
                              "overflow_frac": float(np.maximum(d - 7, 0).sum() / max(1, d.sum())),
                              "tick_kernel_ms": ms, "csr_receipt_ms": csr, "evicts": dg["evicts"],

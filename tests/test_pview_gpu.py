@@ -58,35 +58,32 @@ def test_pview_eviction_bins_match_oracle(case):
 
 
 # the tick kernel's launch forms -- GSP_PV_SPLIT: 0 one 256-lane kernel for every row, 1 rows
-# bucketed by k into four kernels; GSP_PV_SPLITSYNC: 1 exact grids (the bucket sizes read back
-# each tick), 0 grids predicted from the last sizes seen + the overflow kernel (the default, no
-# host wait); GSP_TEST_PV_GRID_CAP caps the predicted grids, so the overflow kernel runs most
-# rows (3) or the tail of every bucket (50)
-# (round 3) a fourth field 0 turns off the one-shard receiver CSR scattered from the send
-# kernel's returned slots (GSP_PV_POS_SCATTER=0: the atomic fill-counter scatter instead)
-@pytest.mark.parametrize("form", ["0:1:0", "1:1:0", "1:0:0", "1:0:3", "1:0:50", "1:0:0:0"])
+# bucketed by k into four kernels on exact grids (the bucket sizes read back each tick; round 5
+# -- they replace round 3's predicted grids and overflow kernel); the second field 0 turns off
+# the one-shard receiver CSR scattered from the send kernel's returned slots
+# (GSP_PV_POS_SCATTER=0: the atomic fill-counter scatter instead)
+def _set_form(monkeypatch, form):
+    split, pos = (form.split(":") + ["1"])[:2]
+    monkeypatch.setenv("GSP_PV_SPLIT", split)
+    monkeypatch.setenv("GSP_PV_POS_SCATTER", pos)
+
+
+@pytest.mark.parametrize("form", ["0", "1", "1:0", "0:0"])
 @pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[4]], ids=lambda c: "n%d_v%d" % c[:2])
 def test_pview_kernel_forms_match_oracle(case, form, monkeypatch):
-    split, sync, cap, pos = (form.split(":") + ["1"])[:4]
-    monkeypatch.setenv("GSP_PV_SPLIT", split)
-    monkeypatch.setenv("GSP_PV_SPLITSYNC", sync)
-    monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
-    monkeypatch.setenv("GSP_PV_POS_SCATTER", pos)
+    _set_form(monkeypatch, form)
     _run_case(case)
 
 
-# the no-wait forms with the event stream on (the overflow kernel runs the
-# rows past a grid; a row run twice would duplicate its event records, which digests and views
-# cannot see) and a per-tick count of the rows the tick kernels ran, which must be every row
-# exactly once (GSP_TEST_PV_COUNT_ROWS=1, gsp_pview_rows_run)
-@pytest.mark.parametrize("form", ["1:0:3", "1:0:50", "1:0:0", "1:1:0", "0:1:0"])
+# every launch form with the event stream on (a row run twice
+# would duplicate its event records, which digests and views cannot see) and a per-tick count
+# of the rows the tick kernels ran, which must be every row exactly once
+# (GSP_TEST_PV_COUNT_ROWS=1, gsp_pview_rows_run)
+@pytest.mark.parametrize("form", ["1", "0"])
 @pytest.mark.parametrize("case", [CASES[1], CASES[3]], ids=lambda c: "n%d_v%d" % c[:2])
 def test_pview_kernel_forms_events_and_rows_run(case, form, monkeypatch):
     from gossip_protocol_amd import _lib
-    split, sync, cap = form.split(":")
-    monkeypatch.setenv("GSP_PV_SPLIT", split)
-    monkeypatch.setenv("GSP_PV_SPLITSYNC", sync)
-    monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
+    _set_form(monkeypatch, form)
     monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
     n, V, f, K, drop, mode, ftick, ppm, seed, ticks = case
     kw = dict(view=V, fanout=f, inbox=K, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
@@ -113,16 +110,13 @@ def test_pview_kernel_forms_events_and_rows_run(case, form, monkeypatch):
 
 
 def test_pview_rows_run_queued_ticks(monkeypatch):
-    """gsp_pview_step(k) queues k ticks without a host wait, every later tick predicted from
-    older bucket sizes: still every row exactly once per tick, with and without the test cap."""
-    for cap in ("0", "50"):
-        monkeypatch.setenv("GSP_TEST_PV_GRID_CAP", cap)
-        monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
-        n = 20000
-        with PviewEngine(n, view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=5,
-                         fail_ppm=50000, seed=3, max_ticks=16) as eng:
-            eng.step(16)
-            assert [eng.rows_run(t) for t in range(1, 17)] == [n] * 16
+    """gsp_pview_step(k) queues k ticks in one call: still every row exactly once per tick."""
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    n = 20000
+    with PviewEngine(n, view=64, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=5,
+                     fail_ppm=50000, seed=3, max_ticks=16) as eng:
+        eng.step(16)
+        assert [eng.rows_run(t) for t in range(1, 17)] == [n] * 16
 
 
 def test_pview_rows_run_needs_the_env():
