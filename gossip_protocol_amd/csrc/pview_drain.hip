@@ -3,27 +3,43 @@
 // The reference drains every queued message (checkMessages, MP1Node.cpp:200-212).  With
 // gsp_pview_params.inbox = 0 the partial view does too: a receiver sent k <= kPvMaxInbox
 // messages runs in the tick kernels as before (they merge all k), and a receiver sent more
-// (a "long" row: the receipt kernel lists it) runs here, one workgroup per row, merging its
-// messages one after the other in ascending sender order into a list that may grow past the
-// view:
-//   1. the segment's senders are sorted ascending (in LDS up to kDrainCap, else in the
-//      workgroup's HBM scratch) and written back in place;
-//   2. the list starts as the own view (ids ascending, values hb << 5 | ts5, kOwnBit set);
-//   3. message j (sender s, payload = s's view of t - 1): each payload entry binary-searches
-//      its id in the list -- found: the max-merge (MP1Node.cpp:247-251); absent: a copy when
-//      fresh and not this node (:282-301) -- and thread 0 does the same for s (hb + 1, ts = t,
-//      or (1, t), :237-243).  The ids of one payload are distinct and s is in no payload of its
-//      own, so every update has its own slot.  The new ids go in by one shift of the list
-//      (their ranks from one block scan);
-//   4. TREMOVE (:339-348), then eviction to V by (age, -hb, id or rotated id): the V-th
-//      smallest 37-bit key age << 32 | (2047 - hb) << 21 | tie key, by a binary search over key
-//      values (37 counting passes), keeps exactly V (the keys are distinct);
-//   5. the new view in id order, the row's counts straight into the tick digest (a long row's
-//      counts overflow the per-row record's 8- and 16-bit fields), its events.
-// The list lives in LDS (kDrainCap entries, 64 KB: two rows per CU) and moves to the
-// workgroup's HBM scratch when a message could overflow it (the hubs: thousands of senders).
-// A list or segment past the scratch (scratch_cap entries) stops the job (GSP_ERR_CAPACITY).
-// Oracle: oracle/pview_oracle.c with inbox = 0 (the same fold over every message).
+// (a "long" row: the receipt kernel lists it by class, pv_drain_class) runs here.
+//
+// The reference merges the k messages one after the other in ascending sender order into a
+// list that may grow past the view (MP1Node.cpp:237-301), then applies TREMOVE (:339-348) and
+// evicts down to V.  Every update of one message touches one id (the payload's ids are
+// distinct, and a sender is in no payload of its own), so the fold is independent per id:
+// the list after message j is, id by id, the ordered fold of that id's updates.  The kernels
+// therefore sort every update of the row by (id, message) and fold each id's run:
+//   1. the segment's senders are sorted ascending (the message order is the sender order, a
+//      JOINREP first);
+//   2. TUPLES, u64: id << 32 | m << 17 | flag << 16 | val (val = hb << 5 | ts5, 16 bits):
+//        m = 0      the list: the own view at the start (flag = 1: in the own view, the
+//                   join count's test), or the list a previous chunk left;
+//        m = 1..kc  message m of the chunk: its payload entries (flag 0; val 0 = a no-op:
+//                   an empty entry or this node's own id) and its sender (flag 1, val 0);
+//      built as runs of Vp = pow2(V) tuples, each sorted by id (views are stored sorted),
+//      the senders' run sorted because the senders are, empty slots ~0 (last);
+//   3. a bottom-up merge-path merge of the runs;
+//   4. the fold of each id's run: cur = 0 (absent); list tuple: cur = val; payload:
+//      cur = pv_merge(cur, val) (MP1Node.cpp:247-251 present, :282-301 absent and fresh);
+//      sender: cur = pv_event(cur) (:237-243).  Ids with cur != 0 are the new list, in id
+//      order, compacted;
+//   5. TREMOVE and eviction to V by (age, -hb, id or rotated id): two 256-bin histogram
+//      passes over the 16-bit prefix age << 11 | (2047 - hb) find the bin holding the V-th
+//      survivor; that bin's members are taken in (rotated) id order -- the list is in id
+//      order already, so a rotation is an offset into it;
+//   6. the new view in id order, the row's counts straight into the tick digest (a long
+//      row's counts overflow the per-row record's 8- and 16-bit fields), its events.
+// Row classes (pview_kernels.hpp pv_drain_class): rows of at most 4,096 / 8,192 / 16,384
+// tuples (k <= 14 / 30 / 62 at V = 256) run in LDS, one buffer merged and folded in place,
+// 256 / 512 / 1024 lanes per row and 4 / 2 / 1 rows per CU (pview_drain_lds_kernel); the
+// rest run in two HBM buffers per workgroup (pview_drain_hbm_kernel), the messages taken in
+// chunks when they do not fit at once, the list carried between chunks as the m = 0 run.  A
+// list past the HBM buffers stops the job (GSP_ERR_CAPACITY).
+// Round 5 replaced a first form that merged the messages one after the other (binary search
+// and shift of the list per message: 19.6 ms per tick over config 5's ticks 1-25).
+// Oracle: oracle/pview_oracle.c with inbox = 0 (the sequential fold over every message).
 #include <cstdint>
 
 #include "join_kernels.hpp"
@@ -36,20 +52,44 @@
 namespace gsp {
 namespace {
 
-constexpr int kDT = 256;                        // threads per drain workgroup (4 waves)
-constexpr int kDrainCap = 8192;                 // LDS list capacity (entries)
-constexpr int kPer = kDrainCap / kDT;           // list entries per lane in the LDS shift
-constexpr uint32_t kOwnBit = 1u << 16;          // the id was in the own view at the start
-constexpr uint64_t kKeyHi = (1ull << 37) - 1;   // eviction keys are 37 bits
+constexpr int kHT = 1024;                       // threads per HBM-kernel workgroup (16 waves)
+constexpr int kHKeys = 2048;                    // HBM kernel: LDS keys for the segment sort
+constexpr uint64_t kNone = ~0ull;               // an empty tuple: sorts last
+constexpr uint32_t kNoId = 0xFFFFFFFFu;
+constexpr int32_t kMaxChunk = 32767;            // messages per chunk: m is 15 bits
+// sender staging word: s << 40 | kind bits | row
+constexpr uint64_t kStageJoinRep = 1ull << 39;  // a JOINREP: node 0's sender entry, no payload
+constexpr uint64_t kStageRemote = 1ull << 38;   // the payload row is a received (remote) row
+constexpr uint64_t kStageRow = (1ull << 38) - 1;
 
+// LDS of one workgroup: CAP tuples (LDS classes: the row's tuple buffer; HBM kernel: segment
+// sort keys), the senders of an LDS row, the eviction histogram, scan and digest words.
+template <int NT, int CAP>
 struct alignas(16) DrainShared {
-    uint32_t ids[kDrainCap];                    // the row's list, ascending ids
-    uint32_t vals[kDrainCap];                   // packed value | kOwnBit
-    uint32_t ins[kPvMaxView + 8];               // insertion points of one message's new ids
-    uint32_t red[2][8];                         // block scan words (two buffers, alternated)
+    static constexpr int kW = NT / 64;
+    uint64_t buf[CAP + CAP / 16];               // LDS rows: skewed (SkewBuf), one pad per 16
+    uint64_t stage[kDrainStage];                // LDS rows: the senders, staged (d_build)
+    uint32_t hist[256];                         // eviction histogram
+    uint32_t red[2][kW];                        // block scan words (two buffers, alternated)
+    uint32_t sel[4];                            // selected bin, tuples still needed from it
+    uint32_t tot[kW][8];                        // per-wave digest counts
 };
 
-// exclusive block scan over the 256 lanes; *total = the sum
+// An LDS tuple buffer indexed with one pad word per 16 tuples: a lane's contiguous run of 16
+// (the merge outputs, the fold's tuples) then starts 17 words after its neighbour's, so the
+// 64-bit reads and writes of a wave hit distinct banks (a stride of 16 words is a 16-way
+// conflict for ds_read_b64 and 32-way for ds_write_b64: MI355X_MICROARCH.md, LDS).
+struct SkewBuf {
+    uint64_t *p;
+    __device__ __forceinline__ uint64_t &operator[](int32_t i) const { return p[i + (i >> 4)]; }
+};
+
+__device__ inline uint64_t d_tuple(uint32_t x, uint32_t m, uint32_t flag, uint32_t v) {
+    return (uint64_t(x) << 32) | uint64_t((m << 17) | (flag << 16) | v);
+}
+
+// exclusive block scan over the workgroup; *total = the sum
+template <int NT>
 __device__ inline uint32_t d_scan(uint32_t v, uint32_t *total, uint32_t *buf) {
     const int32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t incl = wave_incl_scan(v);
@@ -57,7 +97,7 @@ __device__ inline uint32_t d_scan(uint32_t v, uint32_t *total, uint32_t *buf) {
     __syncthreads();
     uint32_t before = 0, all = 0;
 #pragma unroll
-    for (int q = 0; q < kDT / 64; ++q) {
+    for (int q = 0; q < NT / 64; ++q) {
         const uint32_t x = buf[q];
         before += q < wave ? x : 0u;
         all += x;
@@ -66,28 +106,20 @@ __device__ inline uint32_t d_scan(uint32_t v, uint32_t *total, uint32_t *buf) {
     return incl - v + before;
 }
 
+template <int NT>
 __device__ inline uint32_t d_sum(uint32_t v, uint32_t *buf) {
     uint32_t total = 0;
-    (void)d_scan(v, &total, buf);
+    (void)d_scan<NT>(v, &total, buf);
     return total;
-}
-
-// lower bound of x in ids[0, L)
-__device__ inline int32_t d_lower(const uint32_t *ids, int32_t L, uint32_t x) {
-    int32_t lo = 0, hi = L;
-    while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (ids[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    return lo;
 }
 
 // Bitonic sort, ascending, of the P (a power of two) u64 keys at k (LDS or the workgroup's
 // HBM scratch), every thread of the workgroup taking part.
+template <int NT>
 __device__ inline void d_bitonic(uint64_t *k, int32_t P) {
     for (int32_t size = 2; size <= P; size <<= 1)
         for (int32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int32_t i = threadIdx.x; i < P / 2; i += kDT) {
+            for (int32_t i = threadIdx.x; i < P / 2; i += NT) {
                 const int32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
                 const bool up = (lo & size) == 0;
                 const uint64_t x = k[lo], y = k[hi];
@@ -99,9 +131,10 @@ __device__ inline void d_bitonic(uint64_t *k, int32_t P) {
 
 // the segment's (sender, row) pairs sorted by sender, in place (a JOINREP, sender
 // kJoinRepSrc = -1, first: its sender is node 0); keys: P u64 of scratch
+template <int NT>
 __device__ void d_sort_segment(int32_t *src, int32_t *slot, int32_t k, int32_t P, int32_t row0,
                                uint64_t *keys) {
-    for (int32_t i = threadIdx.x; i < P; i += kDT) {
+    for (int32_t i = threadIdx.x; i < P; i += NT) {
         uint64_t key = ~0ull;
         if (i < k) {
             const int32_t s = src[i];
@@ -111,8 +144,8 @@ __device__ void d_sort_segment(int32_t *src, int32_t *slot, int32_t k, int32_t P
         keys[i] = key;
     }
     __syncthreads();
-    d_bitonic(keys, P);
-    for (int32_t i = threadIdx.x; i < k; i += kDT) {
+    d_bitonic<NT>(keys, P);
+    for (int32_t i = threadIdx.x; i < k; i += NT) {
         const uint64_t key = keys[i];
         src[i] = int32_t(uint32_t(key >> 32)) - 1;
         if (slot) slot[i] = int32_t(uint32_t(key));
@@ -120,114 +153,216 @@ __device__ void d_sort_segment(int32_t *src, int32_t *slot, int32_t k, int32_t P
     __syncthreads();
 }
 
-// The row's list: in LDS, or in the HBM scratch (a = current, b = the next message's)
-struct DrainList {
-    int32_t L;                                  // length (block-uniform)
-    bool hbm;
-    uint32_t *aid, *aval, *bid, *bval;
+// Diagnostics (GSP_PV_PROFILE=1): thread 0 adds the cycles of each phase of every 16th row a
+// workgroup runs to prof[slot][8 + min(7, (k - 8) / 8)][phase] (pview_engine.cpp prints them).
+struct DMark {
+    unsigned long long *out = nullptr;
+    uint64_t last = 0;
+    __device__ __forceinline__ void init(unsigned long long *prof, int32_t i, int32_t k) {
+        if (prof && threadIdx.x == 0 && (i & 15) == 0) {
+            const int32_t b = 8 + ((k - 8) / 8 < 7 ? (k - 8) / 8 : 7);
+            out = prof + ((blockIdx.x & 63u) * 16 + uint32_t(b)) * kPvProfPhases;
+            atomicAdd(out + kPvProfPhases - 1, 1ull);
+            last = clock64();
+        }
+    }
+    __device__ __forceinline__ void mark(int phase) {
+        if (out) {
+            const uint64_t now = clock64();
+            atomicAdd(out + phase, (unsigned long long)(now - last));
+            last = now;
+        }
+    }
 };
 
-// Merge one message into the list: sender s, this lane's payload entry e (kPvEmpty: none).
-template <bool kHbm>
-__device__ inline void d_message(DrainShared &sh, DrainList &d, uint32_t r, uint32_t s, uint64_t e,
-                                 uint32_t t5, uint32_t tr) {
-    const int32_t tid = threadIdx.x;
-    uint32_t *ids = kHbm ? d.aid : sh.ids;
-    uint32_t *vals = kHbm ? d.aval : sh.vals;
-    const int32_t L = d.L;
-    const bool ok = e != kPvEmpty;
-    const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
-    int32_t pos = 0;
-    bool ins = false;
-    if (ok) {
-        pos = d_lower(ids, L, x);
-        if (pos < L && ids[pos] == x) {                          // MP1Node.cpp:247-251
-            const uint32_t cur = vals[pos];
-            vals[pos] = (cur & kOwnBit) | pv_merge(cur & 0xFFFFu, v, t5, tr);
-        } else {                                                 // MP1Node.cpp:282-301
-            ins = x != r && ((t5 - v) & 31u) < tr;
-        }
-    }
-    // the sender's entry (MP1Node.cpp:237-243), thread 0
-    int32_t spos = 0;
-    bool sins = false;
-    if (tid == 0) {
-        spos = d_lower(ids, L, s);
-        if (spos < L && ids[spos] == s) {
-            const uint32_t cur = vals[spos];
-            vals[spos] = (cur & kOwnBit) | pv_event(cur & 0xFFFFu, t5);
+// Chunk step 2: the runs of messages [m0, m0 + kc) after the list (padded to Lp), into X;
+// the senders staged in Y.  Returns this lane's count of non-empty payload entries (the
+// digest's merges).
+template <int NT, class P>
+__device__ __forceinline__ uint32_t d_build(const PviewTickArgs &a, P X, uint64_t *Y, int32_t L,
+                                            int32_t Lp, int32_t m0, int32_t kc, int32_t Vp, int32_t lgV,
+                                            const int32_t *src, const int32_t *slot, uint32_t r) {
+    const int32_t tid = threadIdx.x, V = a.view;
+    for (int32_t i = tid; i < kc; i += NT) {                     // stage the senders in Y
+        const int32_t s = src[m0 + i];
+        uint64_t w;
+        if (s == kJoinRepSrc) {
+            w = kStageJoinRep;
         } else {
-            sins = true;
+            const int32_t sl = slot ? slot[m0 + i] : s - a.row0;
+            w = (uint64_t(uint32_t(s)) << 40) | (sl >= 0 ? uint64_t(sl) : (kStageRemote | uint64_t(-int64_t(sl) - 1)));
         }
+        Y[i] = w;
     }
-    // ranks of the new ids: the payload's in lane (= id) order, the sender's among them -- one
-    // scan of three 11-bit counts (payload inserts, those below s, the sender's insert)
-    uint32_t tot = 0;
-    const uint32_t ex = d_scan((ins ? 1u : 0u) | ((ins && x < s) ? 1u << 11 : 0u) | (sins ? 1u << 22 : 0u),
-                               &tot, sh.red[0]);
-    const bool s_ins = (tot >> 22) != 0;
-    const int32_t s_rank = int32_t((tot >> 11) & 0x7FFu);
-    const int32_t m = int32_t(tot & 0x7FFu) + (s_ins ? 1 : 0);
-    if (m == 0) {
-        __syncthreads();                                         // red[0] is read to its end
-        return;
-    }
-    const int32_t rank = int32_t(ex & 0x7FFu) + ((s_ins && s < x) ? 1 : 0);
-    if (ins) sh.ins[rank] = uint32_t(pos);
-    if (tid == 0 && s_ins) sh.ins[s_rank] = uint32_t(spos);
-    __syncthreads();                                             // insertion points, updates
-    // the shift: old entry i moves up by the number of new ids inserted at or below it
-    if constexpr (!kHbm) {
-        const int32_t per = (L + kDT - 1) / kDT, c0 = tid * per;
-        uint32_t rid[kPer], rv[kPer];
-        int32_t q = d_lower(sh.ins, m, uint32_t(c0) + 1u);       // inserts with position <= c0
+    for (int32_t i = L + tid; i < Lp; i += NT) X[i] = kNone;
+    __syncthreads();
+    const int32_t np = kc << lgV;                                // payload tuples
+    const int32_t nt = np + ((kc + Vp - 1) >> lgV << lgV);       // + the senders' runs
+    uint32_t merged = 0;
+    constexpr int kB = 8;                                        // loads in flight per lane
+    for (int32_t q0 = 0; q0 < nt; q0 += kB * NT) {
+        uint64_t e[kB];
+        uint32_t mi[kB];
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            rid[i] = rv[i] = 0;
-            if (i < per && c0 + i < L) { rid[i] = ids[c0 + i]; rv[i] = vals[c0 + i]; }
-        }
-        __syncthreads();                                         // every read before any write
-#pragma unroll
-        for (int i = 0; i < kPer; ++i) {
-            const int32_t at = c0 + i;
-            if (i < per && at < L) {
-                while (q < m && int32_t(sh.ins[q]) <= at) ++q;
-                ids[at + q] = rid[i];
-                vals[at + q] = rv[i];
+        for (int u = 0; u < kB; ++u) {
+            const int32_t q = q0 + u * NT + tid;
+            e[u] = kPvEmpty;
+            mi[u] = 0;
+            if (q < np) {
+                const int32_t m = q >> lgV, pos = q & (Vp - 1);
+                mi[u] = uint32_t(m);
+                const uint64_t w = Y[m];
+                if (pos < V && !(w & kStageJoinRep)) {
+                    const int64_t row = int64_t(w & kStageRow);
+                    const uint64_t *p = (w & kStageRemote) ? a.remote : a.prev;
+                    e[u] = p[row * V + pos];
+                }
+            } else if (q < nt && q - np < kc) {
+                mi[u] = uint32_t(q - np);
+                e[u] = Y[q - np];                                // the staging word
             }
         }
-        if (ins) { ids[pos + rank] = x; vals[pos + rank] = v; }
-        if (tid == 0 && s_ins) { ids[spos + s_rank] = s; vals[spos + s_rank] = pv_event(0u, t5); }
-    } else {
-        for (int32_t i = tid; i < L; i += kDT) {
-            const int32_t q = d_lower(sh.ins, m, uint32_t(i) + 1u);
-            d.bid[i + q] = ids[i];
-            d.bval[i + q] = vals[i];
+#pragma unroll
+        for (int u = 0; u < kB; ++u) {
+            const int32_t q = q0 + u * NT + tid;
+            if (q >= nt) continue;
+            uint64_t key = kNone;
+            if (q < np) {
+                if (e[u] != kPvEmpty) {
+                    merged++;
+                    const uint32_t x = uint32_t(e[u] >> 32), v = uint32_t(e[u]) & 0xFFFFu;
+                    key = d_tuple(x, mi[u] + 1u, 0u, x == r ? 0u : v);
+                }
+            } else if (q - np < kc) {
+                const uint32_t s = (e[u] & kStageJoinRep) ? 0u : uint32_t(e[u] >> 40);
+                key = d_tuple(s, mi[u] + 1u, 1u, 0u);
+            }
+            X[Lp + q] = key;
         }
-        if (ins) { d.bid[pos + rank] = x; d.bval[pos + rank] = v; }
-        if (tid == 0 && s_ins) { d.bid[spos + s_rank] = s; d.bval[spos + s_rank] = pv_event(0u, t5); }
-        uint32_t *ti = d.aid, *tv = d.aval;
-        d.aid = d.bid; d.aval = d.bval; d.bid = ti; d.bval = tv;
     }
-    d.L = L + m;
+    __syncthreads();
+    return merged;
+}
+
+// Chunk step 3 (HBM kernel): merge-path merges of the sorted runs of width Vp, X <-> Y;
+// returns the offset of the sorted buffer.
+__device__ __forceinline__ int64_t d_merge_runs(uint64_t *base, int64_t C, int64_t xo, int32_t N, int32_t Vp) {
+    const int32_t tid = threadIdx.x;
+    int32_t E = 2;                                               // outputs per lane and pass
+    while (E < 16 && int64_t(E) * kHT < N) E <<= 1;
+    for (int32_t w = Vp; w < N; w <<= 1) {
+        const uint64_t *X = base + xo;
+        uint64_t *Y = base + (C - xo);
+        const int32_t Ew = E < 2 * w ? E : 2 * w;                // divides 2w: one pair per piece
+        for (int32_t d0 = tid * Ew; d0 < N; d0 += kHT * Ew) {
+            const int32_t p0 = d0 & ~(2 * w - 1);
+            const int32_t a1 = p0 + w < N ? p0 + w : N, b1 = p0 + 2 * w < N ? p0 + 2 * w : N;
+            const int32_t na = a1 - p0, nb = b1 - a1, d = d0 - p0;
+            const uint64_t *A = X + p0, *B = X + a1;
+            int32_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+            while (lo < hi) {                                    // merge path: A first on ties
+                const int32_t mid = (lo + hi) >> 1;
+                if (A[mid] <= B[d - 1 - mid]) lo = mid + 1; else hi = mid;
+            }
+            int32_t i = lo, j = d - lo;
+            uint64_t va = i < na ? A[i] : kNone, vb = j < nb ? B[j] : kNone;
+            const int32_t n = b1 - d0 < Ew ? b1 - d0 : Ew;
+            for (int32_t q = 0; q < n; ++q) {
+                const bool ta = j >= nb || (i < na && va <= vb);
+                Y[d0 + q] = ta ? va : vb;
+                if (ta) { ++i; va = i < na ? A[i] : kNone; }
+                else { ++j; vb = j < nb ? B[j] : kNone; }
+            }
+        }
+        __syncthreads();
+        xo = C - xo;
+    }
+    return xo;
+}
+
+// The fold of one id's run S[i, ...) (sorted tuples): the entry's value (0: absent) and
+// whether it was in the list before (own).
+template <class P>
+__device__ __forceinline__ uint32_t d_fold_run(const P &S, int32_t i, int32_t N, uint64_t t, uint32_t x,
+                                               uint32_t t5, uint32_t tr, uint32_t *own) {
+    uint32_t cur = 0, o = 0;
+    for (int32_t j = i; j < N; ++j) {                            // the id's run, in message order
+        const uint64_t u = j == i ? t : S[j];
+        if (uint32_t(u >> 32) != x) break;
+        const uint32_t lo = uint32_t(u), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
+        if (m == 0) {
+            if (v) { cur = v; o = fl; }
+        } else if (fl) {
+            cur = pv_event(cur, t5);                             // MP1Node.cpp:237-243
+        } else {
+            cur = pv_merge(cur, v, t5, tr);                      // MP1Node.cpp:247-251, 282-301
+        }
+    }
+    *own = o;
+    return cur;
+}
+
+// Chunk step 4 (HBM kernel): each id's run folded (sorted tuples S[0, N)); the new list,
+// compacted in id order, into S.  D: the other buffer.  Returns the list length.
+template <class Sh>
+__device__ __forceinline__ int32_t d_fold(Sh &sh, uint64_t *S, uint64_t *D, int32_t N, uint32_t t5,
+                                          uint32_t tr) {
+    const int32_t tid = threadIdx.x;
+    const int32_t F = (N + kHT - 1) / kHT, i0 = tid * F, i1 = i0 + F < N ? i0 + F : N;
+    uint32_t cnt = 0;
+    uint32_t prev = i0 > 0 && i0 < N ? uint32_t(S[i0 - 1] >> 32) : kNoId;
+    for (int32_t i = i0; i < i1; ++i) {
+        const uint64_t t = S[i];
+        const uint32_t x = uint32_t(t >> 32);
+        if (x == kNoId) break;                                   // the empty tuples: the tail
+        if (i > 0 && x == prev) continue;
+        prev = x;
+        uint32_t own;
+        const uint32_t cur = d_fold_run(S, i, N, t, x, t5, tr, &own);
+        if (cur) D[i0 + int32_t(cnt++)] = d_tuple(x, 0u, own, cur);
+    }
+    uint32_t L = 0;
+    const uint32_t at = d_scan<kHT>(cnt, &L, sh.red[0]);         // S read to its end by now
+    for (uint32_t q = 0; q < cnt; ++q) S[at + q] = D[i0 + int32_t(q)];
+    __syncthreads();
+    return int32_t(L);
+}
+
+// Step 5's bin selection (wave 0): the first bin where the running count reaches need;
+// sh.sel = {bin, tuples still needed from it}
+template <class Sh>
+__device__ inline void d_select(Sh &sh, uint32_t need) {
+    if (threadIdx.x < 64) {
+        const int32_t l = threadIdx.x;
+        uint32_t h[4], s = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { h[q] = sh.hist[4 * l + q]; s += h[q]; }
+        const uint32_t incl = wave_incl_scan(s);
+        const uint64_t bal = __ballot(incl >= need);
+        const int32_t fl = bal ? __ffsll((unsigned long long)bal) - 1 : 63;
+        if (l == fl) {
+            uint32_t cum = incl - s;
+            int32_t b = 0;
+            for (; b < 3; ++b) {
+                if (cum + h[b] >= need) break;
+                cum += h[b];
+            }
+            sh.sel[0] = uint32_t(4 * l + b);
+            sh.sel[1] = need - cum;
+        }
+    }
     __syncthreads();
 }
 
-// eviction key of a surviving entry: (age, -hb, tie key) ascending = the order entries are kept
-__device__ inline uint64_t d_key(uint32_t x, uint32_t v, uint32_t t5, uint32_t mrot, uint32_t n, bool rot) {
-    const uint32_t age = (t5 - v) & 31u, hb = v >> 5;
-    const uint32_t tk = rot ? (x >= mrot ? x - mrot : x + n - mrot) : x;
-    return (uint64_t(age) << 32) | (uint64_t(2047u - hb) << 21) | uint64_t(tk);
+__device__ inline uint32_t d_prefix(uint32_t v, uint32_t t5) {   // age << 11 | (2047 - hb)
+    return (((t5 - v) & 31u) << 11) | (2047u - (v >> 5));
 }
 
-// TREMOVE, eviction, the new view, the row's digest counts and events (steps 4-5).
-template <bool kEv>
-__device__ void d_finish(const PviewTickArgs &a, DrainShared &sh, const DrainList &d, int32_t lr,
-                         uint32_t r, int32_t k, uint32_t merged) {
-    const int32_t tid = threadIdx.x;
-    const uint32_t *ids = d.hbm ? d.aid : sh.ids;
-    const uint32_t *vals = d.hbm ? d.aval : sh.vals;
-    const int32_t L = d.L, V = a.view;
+// Steps 5-6 over the list S[0, L) (x << 32 | own << 16 | val).
+template <bool kEv, int NT, class Sh, class P>
+__device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, int32_t L,
+                                         int32_t lr, uint32_t r, int32_t k, uint32_t merged, DMark &pm) {
+    const int32_t tid = threadIdx.x, V = a.view;
     const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove);
     const uint64_t Sj = pv_seed(1, t, r), Sr = pv_seed(2, t, r), Se = pv_seed(3, t, r);
     const bool rot = a.evict_rot != 0;
@@ -236,88 +371,157 @@ __device__ void d_finish(const PviewTickArgs &a, DrainShared &sh, const DrainLis
     uint32_t joins = 0, removes = 0, surv = 0;
     uint64_t hsum = 0;
     // joins (not in the own view at the start) and TREMOVE (MP1Node.cpp:339-348)
-    for (int32_t i = tid; i < L; i += kDT) {
-        const uint32_t val = vals[i], x = ids[i], v = val & 0xFFFFu;
-        const bool jn = !(val & kOwnBit), rm = ((t5 - v) & 31u) >= tr;
-        joins += jn ? 1u : 0u;
-        removes += rm ? 1u : 0u;
-        surv += rm ? 0u : 1u;
-        if (jn) hsum += pv_hash(uint32_t(Sj), x);
-        if (rm) hsum += pv_hash(uint32_t(Sr), x);
-    }
-    if (ev) {
-        for (int32_t base = 0; base < L; base += kDT) {          // wave-uniform trips
-            const int32_t i = base + tid;
-            uint32_t val = 0, x = 0;
-            if (i < L) { val = vals[i]; x = ids[i]; }
-            const bool jn = i < L && !(val & kOwnBit) && (a.ev.kinds & GSP_EVENTS_JOIN);
-            const bool rm = i < L && ((t5 - (val & 0xFFFFu)) & 31u) >= tr && (a.ev.kinds & GSP_EVENTS_REMOVE);
-            uint64_t p = wave_reserve_events(ev_stripe_count(a.ev), (jn ? 1u : 0u) + (rm ? 1u : 0u));
+    for (int32_t base = 0; base < L; base += NT) {               // wave-uniform trips
+        const int32_t i = base + tid;
+        bool jn = false, rm = false;
+        uint32_t x = 0;
+        if (i < L) {
+            const uint64_t e = S[i];
+            x = uint32_t(e >> 32);
+            const uint32_t v = uint32_t(e) & 0xFFFFu;
+            jn = !((uint32_t(e) >> 16) & 1u);
+            rm = ((t5 - v) & 31u) >= tr;
+            joins += jn ? 1u : 0u;
+            removes += rm ? 1u : 0u;
+            surv += rm ? 0u : 1u;
+            if (jn) hsum += pv_hash(uint32_t(Sj), x);
+            if (rm) hsum += pv_hash(uint32_t(Sr), x);
+        }
+        if (ev) {
+            const bool ej = jn && (a.ev.kinds & GSP_EVENTS_JOIN), er = rm && (a.ev.kinds & GSP_EVENTS_REMOVE);
+            uint64_t p = wave_reserve_events(ev_stripe_count(a.ev), (ej ? 1u : 0u) + (er ? 1u : 0u));
             unsigned long long *eb = ev_stripe_buf(a.ev);
-            if (jn) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(1u, t, r, x); ++p; }
-            if (rm) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(2u, t, r, x); }
+            if (ej) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(1u, t, r, x); ++p; }
+            if (er) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(2u, t, r, x); }
         }
     }
-    const uint32_t C = d_sum(surv, sh.red[0]);
-    // the V-th smallest key: smallest T with #{key <= T} >= V (keys are distinct)
-    uint64_t T = kKeyHi;
+    const uint32_t C = d_sum<NT>(surv, sh.red[0]);
+    pm.mark(5);
+    // the V-th survivor's prefix bin T16 and how many of that bin are kept (need2); every
+    // survivor with a smaller prefix is kept
+    uint32_t T16 = 0x10000u, need2 = 0;
     if (int32_t(C) > V) {
-        uint64_t lo = 0, hi = kKeyHi;
-        int b = 1;
-        while (lo < hi) {                                        // block-uniform
-            const uint64_t mid = lo + ((hi - lo) >> 1);
-            uint32_t c = 0;
-            for (int32_t i = tid; i < L; i += kDT) {
-                const uint32_t v = vals[i] & 0xFFFFu;
-                c += (((t5 - v) & 31u) < tr && d_key(ids[i], v, t5, mrot, uint32_t(a.n), rot) <= mid) ? 1u : 0u;
+        for (int pass = 0; pass < 2; ++pass) {
+            if (tid < 256) sh.hist[tid] = 0;
+            __syncthreads();
+            const uint32_t hi = pass ? T16 : 0u;
+            for (int32_t i = tid; i < L; i += NT) {
+                const uint32_t v = uint32_t(S[i]) & 0xFFFFu;
+                if (((t5 - v) & 31u) >= tr) continue;
+                const uint32_t p = d_prefix(v, t5);
+                if (pass == 0) atomicAdd(&sh.hist[p >> 8], 1u);
+                else if ((p >> 8) == hi) atomicAdd(&sh.hist[p & 255u], 1u);
             }
-            if (d_sum(c, sh.red[b]) >= uint32_t(V)) hi = mid; else lo = mid + 1;
-            b ^= 1;
+            __syncthreads();
+            d_select(sh, pass ? need2 : uint32_t(V));
+            if (pass == 0) { T16 = sh.sel[0]; need2 = sh.sel[1]; }
+            else { T16 = (T16 << 8) | sh.sel[0]; need2 = sh.sel[1]; }
+            __syncthreads();                                     // sel / hist reused
         }
-        T = lo;
     }
-    // the kept entries in id order, evictions counted
+    pm.mark(6);
+    // the kept entries in id order: contiguous pieces per lane.  The T16 bin's members are
+    // kept in (rotated) id order: member rank rho (id order) -> (rho - MB) mod c2, MB = the
+    // members below the rotation point
+    const int32_t F = (L + NT - 1) / NT, i0 = tid * F, i1 = i0 + F < L ? i0 + F : L;
+    uint32_t mc = 0, mb = 0;
+    if (T16 < 0x10000u)
+        for (int32_t i = i0; i < i1; ++i) {
+            const uint64_t e = S[i];
+            const uint32_t v = uint32_t(e) & 0xFFFFu;
+            if (((t5 - v) & 31u) < tr && d_prefix(v, t5) == T16) {
+                mc++;
+                mb += uint32_t(e >> 32) < mrot ? 1u : 0u;
+            }
+        }
+    uint32_t c2 = 0, MB = 0;
+    const uint32_t rho0 = d_scan<NT>(mc, &c2, sh.red[1]);
+    MB = d_sum<NT>(mb, sh.red[0]);
+    uint32_t kept = 0;
+    {
+        uint32_t rho = rho0;
+        for (int32_t i = i0; i < i1; ++i) {
+            const uint32_t v = uint32_t(S[i]) & 0xFFFFu;
+            if (((t5 - v) & 31u) >= tr) continue;
+            const uint32_t p = d_prefix(v, t5);
+            if (p < T16) kept++;
+            else if (p == T16) {
+                const uint32_t rr = rho >= MB ? rho - MB : rho + c2 - MB;
+                kept += rr < need2 ? 1u : 0u;
+                rho++;
+            }
+        }
+    }
+    uint32_t W = 0;
+    const uint32_t w0 = d_scan<NT>(kept, &W, sh.red[1]);
     uint64_t *out = a.cur + int64_t(lr) * V;
     uint32_t evicts = 0;
-    int32_t w = 0, b = 0;
-    for (int32_t base = 0; base < L; base += kDT) {
-        const int32_t i = base + tid;
-        uint32_t x = 0, v = 0;
-        bool keep = false, evict = false;
-        if (i < L) {
-            x = ids[i];
-            v = vals[i] & 0xFFFFu;
-            if (((t5 - v) & 31u) < tr) {
-                keep = d_key(x, v, t5, mrot, uint32_t(a.n), rot) <= T;
-                evict = !keep;
+    {
+        uint32_t rho = rho0, w = w0;
+        for (int32_t i = i0; i < i1; ++i) {
+            const uint64_t e = S[i];
+            const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
+            if (((t5 - v) & 31u) >= tr) continue;
+            const uint32_t p = d_prefix(v, t5);
+            bool keep = p < T16;
+            if (p == T16) {
+                const uint32_t rr = rho >= MB ? rho - MB : rho + c2 - MB;
+                keep = rr < need2;
+                rho++;
+            }
+            if (keep) {
+                __builtin_nontemporal_store((uint64_t(x) << 32) | uint64_t(v), out + w++);
+            } else {
+                evicts++;
+                hsum += pv_hash(uint32_t(Se), x);
             }
         }
-        uint32_t tot = 0;
-        const uint32_t pos = d_scan(keep ? 1u : 0u, &tot, sh.red[b]);
-        b ^= 1;
-        if (keep) __builtin_nontemporal_store((uint64_t(x) << 32) | uint64_t(v), out + w + int32_t(pos));
-        if (evict) { evicts++; hsum += pv_hash(uint32_t(Se), x); }
-        if (ev && (a.ev.kinds & GSP_EVENTS_EVICT)) {
-            uint64_t p = wave_reserve_events(ev_stripe_count(a.ev), evict ? 1u : 0u);
-            if (evict && int64_t(p) < a.ev.cap) ev_stripe_buf(a.ev)[p] = event_record(3u, t, r, x);
-        }
-        w += int32_t(tot);
     }
-    for (int32_t i = w + tid; i < V; i += kDT) __builtin_nontemporal_store(kPvEmpty, out + i);
-    // the row's counts: straight into the tick digest (its per-row record stays zero)
-    const uint32_t jr = d_sum(joins, sh.red[b]);
-    b ^= 1;
-    const uint32_t rm = d_sum(removes, sh.red[b]);
-    b ^= 1;
-    const uint32_t evs = d_sum(evicts, sh.red[b]);
-    b ^= 1;
-    const uint32_t mg = d_sum(merged, sh.red[b]);
-    b ^= 1;
-    const uint64_t h_lo = d_sum(uint32_t(hsum) & 0xFFFFu, sh.red[b]);
-    b ^= 1;
-    const uint64_t h_mid = d_sum((uint32_t(hsum) >> 16) & 0xFFFFu, sh.red[b]);
-    b ^= 1;
-    const uint64_t h_hi = d_sum(uint32_t(hsum >> 32), sh.red[b]);
+    if (ev && (a.ev.kinds & GSP_EVENTS_EVICT)) {                 // a second pass, wave-uniform trips
+        uint32_t rho = rho0;
+        for (int32_t q = 0; q < F; ++q) {
+            const int32_t i = i0 + q;
+            bool evict = false;
+            uint32_t x = 0;
+            if (i < i1) {
+                const uint64_t e = S[i];
+                x = uint32_t(e >> 32);
+                const uint32_t v = uint32_t(e) & 0xFFFFu;
+                if (((t5 - v) & 31u) < tr) {
+                    const uint32_t p = d_prefix(v, t5);
+                    evict = p > T16;
+                    if (p == T16) {
+                        const uint32_t rr = rho >= MB ? rho - MB : rho + c2 - MB;
+                        evict = rr >= need2;
+                        rho++;
+                    }
+                }
+            }
+            uint64_t pe = wave_reserve_events(ev_stripe_count(a.ev), evict ? 1u : 0u);
+            if (evict && int64_t(pe) < a.ev.cap) ev_stripe_buf(a.ev)[pe] = event_record(3u, t, r, x);
+        }
+    }
+    for (int32_t i = int32_t(W) + tid; i < V; i += NT) __builtin_nontemporal_store(kPvEmpty, out + i);
+    pm.mark(7);
+    // the row's counts: straight into the tick digest (its per-row record stays zero) --
+    // joins, removes, evictions, merges and the hash (16 + 16 + 32 bits), one reduction
+    {
+        const uint32_t part[7] = {joins, removes, evicts, merged, uint32_t(hsum) & 0xFFFFu,
+                                  (uint32_t(hsum) >> 16) & 0xFFFFu, uint32_t(hsum >> 32)};
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            const uint32_t w = wave_sum32(part[q]);
+            if ((tid & 63) == 0) sh.tot[tid >> 6][q] = w;
+        }
+    }
+    __syncthreads();
+    uint32_t sum[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (tid < 64) {                                              // wave 0: lane w reads wave w's
+#pragma unroll
+        for (int q = 0; q < 7; ++q) sum[q] = wave_sum32(tid < NT / 64 ? sh.tot[tid][q] : 0u);
+    }
+    const uint32_t jr = sum[0], rm = sum[1], evs = sum[2], mg = sum[3];
+    const uint64_t h_lo = sum[4], h_mid = sum[5], h_hi = sum[6];
     if (tid == 0) {
         unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
         atomicAdd(dig + kPvRounds, 1ull);
@@ -329,16 +533,169 @@ __device__ void d_finish(const PviewTickArgs &a, DrainShared &sh, const DrainLis
         const uint64_t h = h_lo + (h_mid << 16) + (h_hi << 32) + uint64_t(jr) * Sj + uint64_t(rm) * Sr +
                            uint64_t(evs) * Se;
         atomicAdd(dig + kPvHash, (unsigned long long)h);
-        a.len_cur[lr] = w;
+        a.len_cur[lr] = int32_t(W);
         // alive at every tick since it started (pre-joined: ticks 1..t)
         const int32_t st = a.start_tick ? a.start_tick[r] : 0;
         a.own_hb[lr] = int32_t(t) - (st > 0 ? st - 1 : 0);
     }
     if (tid < 16 && tid != 3) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;   // w3: the send kernel's
+    pm.mark(8);
 }
 
-template <bool kEv>
-__device__ void d_row(const PviewTickArgs &a, DrainShared &sh, int32_t lr, uint32_t *scratch) {
+// The list's first form: the own view, this node itself and zero values left out, as list
+// tuples (flag 1: in the own view) at X[0, L); returns L.
+template <int NT, class Sh, class P>
+__device__ __forceinline__ int32_t d_own(const PviewTickArgs &a, Sh &sh, P X, int32_t lr, uint32_t r) {
+    const int32_t tid = threadIdx.x, V = a.view;
+    const uint64_t e = tid < V ? a.prev[int64_t(lr) * V + tid] : kPvEmpty;
+    const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
+    const bool keep = e != kPvEmpty && x != r && v != 0u;
+    uint32_t tot = 0;
+    const uint32_t pos = d_scan<NT>(keep ? 1u : 0u, &tot, sh.red[1]);
+    if (keep) X[pos] = d_tuple(x, 0u, 1u, v);
+    __syncthreads();
+    return int32_t(tot);
+}
+
+// ---- LDS classes: the row's N <= CAP tuples in one LDS buffer, merged in place ----------
+
+// Compare-exchange of two u64 registers (ascending)
+__device__ __forceinline__ void d_cx(uint64_t &x, uint64_t &y) {
+    const uint64_t lo = x < y ? x : y, hi = x < y ? y : x;
+    x = lo;
+    y = hi;
+}
+
+// Merge levels in place: each lane finds the co-rank of its E = CAP / NT outputs, loads the E
+// tuples of each input from there (two batches of independent LDS reads), keeps the E
+// smallest of the 2E (a bitonic half-cleaner: a[q] against b[E-1-q]) and sorts that bitonic
+// sequence in registers (log2 E stages); the workgroup waits, then the lanes write their
+// outputs over the inputs (Vp >= 8: a lane's outputs lie in one pair of runs).
+template <int NT, int E, class P>
+__device__ __forceinline__ void d_merge_ip(P X, int32_t N, int32_t Vp) {
+    static_assert((E & (E - 1)) == 0, "E is a power of two");
+    const int32_t d0 = int32_t(threadIdx.x) * E;
+    for (int32_t w = Vp; w < N; w <<= 1) {
+        uint64_t o[E];
+        int32_t n = 0;
+        if (d0 < N) {
+            const int32_t p0 = d0 & ~(2 * w - 1);
+            const int32_t a1 = p0 + w < N ? p0 + w : N, b1 = p0 + 2 * w < N ? p0 + 2 * w : N;
+            const int32_t na = a1 - p0, nb = b1 - a1, d = d0 - p0;
+            int32_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+            while (lo < hi) {                                    // merge path: A first on ties
+                const int32_t mid = (lo + hi) >> 1;
+                if (X[p0 + mid] <= X[a1 + d - 1 - mid]) lo = mid + 1; else hi = mid;
+            }
+            const int32_t i = lo, j = d - lo;
+            uint64_t bq[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) {                        // the next E of each input
+                o[q] = i + q < na ? X[p0 + i + q] : kNone;
+                bq[q] = j + q < nb ? X[a1 + j + q] : kNone;
+            }
+#pragma unroll
+            for (int q = 0; q < E; ++q) {                        // the E smallest: bitonic
+                const uint64_t y = bq[E - 1 - q];
+                o[q] = o[q] < y ? o[q] : y;
+            }
+#pragma unroll
+            for (int h = E / 2; h > 0; h >>= 1)                  // bitonic sort, ascending
+#pragma unroll
+                for (int q = 0; q < E; ++q)
+                    if ((q & h) == 0) d_cx(o[q], o[q + h]);
+            n = b1 - d0 < E ? b1 - d0 : E;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < E; ++q)
+            if (q < n) X[d0 + q] = o[q];
+        __syncthreads();
+    }
+}
+
+// Each id's run folded in place.  Pass 1: lane t loads its F tuples into registers (one batch
+// of independent LDS reads), folds the runs that start among them in registers -- a run that
+// continues past them is walked on in LDS (rare) -- and writes each run's result over the
+// run's first tuple (id kept: a neighbour only reads a run head to see that its own run has
+// ended; results have m = 0, the runs' other tuples m >= 1).  Pass 2: after a barrier the lane
+// loads its results and, after the scan's barrier, writes them compacted in id order.
+// Returns the list length.
+template <int NT, int F, class Sh, class P>
+__device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5, uint32_t tr) {
+    const int32_t i0 = int32_t(threadIdx.x) * F;
+    uint64_t tu[F];
+#pragma unroll
+    for (int q = 0; q < F; ++q) tu[q] = i0 + q < N ? S[i0 + q] : kNone;
+    const uint32_t prev = i0 > 0 && i0 < N ? uint32_t(S[i0 - 1] >> 32) : kNoId;
+    uint32_t cnt = 0;
+    uint32_t rx = kNoId, cur = 0, own = 0;                       // the run being folded
+    int32_t at0 = -1;                                            // its first tuple (this lane's)
+#pragma unroll
+    for (int q = 0; q < F; ++q) {
+        const uint32_t x = uint32_t(tu[q] >> 32);
+        const uint32_t px = q == 0 ? prev : uint32_t(tu[q > 0 ? q - 1 : 0] >> 32);
+        if (x != px) {                                           // a run starts here
+            rx = x;
+            cur = 0;
+            own = 0;
+            at0 = x != kNoId ? q : -1;
+        }
+        if (at0 >= 0) {                                          // a run of this lane
+            const uint32_t lo = uint32_t(tu[q]), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
+            if (m == 0) {
+                if (v) { cur = v; own = fl; }
+            } else if (fl) {
+                cur = pv_event(cur, t5);                         // MP1Node.cpp:237-243
+            } else {
+                cur = pv_merge(cur, v, t5, tr);                  // MP1Node.cpp:247-251, 282-301
+            }
+        }
+        (void)rx;
+        const uint32_t nx = q + 1 < F ? uint32_t(tu[q + 1 < F ? q + 1 : q] >> 32) : kNoId;
+        const bool ends = q + 1 < F ? nx != x : true;
+        if (ends && at0 >= 0) {
+            if (q + 1 == F) {                                    // may continue past this lane
+                for (int32_t j = i0 + F; j < N; ++j) {
+                    const uint64_t u = S[j];
+                    if (uint32_t(u >> 32) != x) break;
+                    const uint32_t lo = uint32_t(u), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
+                    if (m == 0) {
+                        if (v) { cur = v; own = fl; }
+                    } else if (fl) {
+                        cur = pv_event(cur, t5);
+                    } else {
+                        cur = pv_merge(cur, v, t5, tr);
+                    }
+                }
+            }
+            S[i0 + at0] = d_tuple(x, 0u, cur ? own : 0u, cur);   // cur = 0: absent
+            cnt += cur ? 1u : 0u;
+            at0 = -1;
+        }
+    }
+    __syncthreads();                                             // every run folded
+    uint64_t res[F];
+#pragma unroll
+    for (int q = 0; q < F; ++q) {
+        const int32_t i = i0 + q;
+        const uint64_t t = i < N ? S[i] : kNone;
+        const uint32_t lo = uint32_t(t);
+        res[q] = (t != kNone && (lo >> 17) == 0u && (lo & 0xFFFFu) != 0u) ? t : 0ull;
+    }
+    uint32_t L = 0;
+    uint32_t at = d_scan<NT>(cnt, &L, sh.red[0]);                // every result loaded by now
+#pragma unroll
+    for (int q = 0; q < F; ++q)
+        if (res[q]) S[at++] = res[q];
+    __syncthreads();
+    return int32_t(L);
+}
+
+// One row of an LDS class, every message in one pass.
+template <bool kEv, int NT, int CAP>
+__device__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, int32_t lr, int32_t it) {
+    constexpr int E = CAP / NT;
     const int32_t tid = threadIdx.x;
     const uint32_t r = uint32_t(a.row0 + lr);
     if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);       // tests: each row exactly once
@@ -349,94 +706,148 @@ __device__ void d_row(const PviewTickArgs &a, DrainShared &sh, int32_t lr, uint3
     }
     const int32_t V = a.view;
     const uint32_t t5 = uint32_t(a.tick) & 31u, tr = uint32_t(a.tremove);
+    const int32_t o0 = a.csr_off[lr];
+    const int32_t k = a.csr_off[lr + 1] - o0;                    // <= kDrainStage (the class)
+    int32_t *src = a.csr_src + o0;
+    int32_t *slot = a.csr_slot ? a.csr_slot + o0 : nullptr;
+    DMark pm;
+    pm.init(a.prof, it, k);
+    int32_t P = 1;
+    while (P < k) P <<= 1;
+    d_sort_segment<NT>(src, slot, k, P, a.row0, sh.buf);         // 1. ascending senders
+    pm.mark(0);
+    int32_t lgV = 0;
+    while ((1 << lgV) < V) ++lgV;
+    const int32_t Vp = 1 << lgV;
+    const SkewBuf X{sh.buf};
+    const int32_t L0 = d_own<NT>(a, sh, X, lr, r);               // <= V: padded to Vp
+    pm.mark(1);
+    const uint32_t merged = d_build<NT>(a, X, sh.stage, L0, Vp, 0, k, Vp, lgV, src, slot, r);
+    pm.mark(2);
+    const int32_t N = Vp + (k << lgV) + ((k + Vp - 1) >> lgV << lgV);
+    d_merge_ip<NT, E>(X, N, Vp);
+    pm.mark(3);
+    const int32_t L = d_fold_ip<NT, E>(sh, X, N, t5, tr);
+    pm.mark(4);
+    d_finish<kEv, NT>(a, sh, X, L, lr, r, k, merged, pm);
+}
+
+// Persistent over the class's rows: workgroup b takes rows b, b + grid, ...
+template <bool kEv, int NT, int CAP, int kCls>
+__global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a) {
+    __shared__ DrainShared<NT, CAP> sh;
+    const int32_t cnt = a.long_list[kCls];
+    const int32_t *list = a.long_list + 4 + int64_t(kCls) * a.rows;
+    for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
+        d_row_lds<kEv, NT, CAP>(a, sh, list[i], (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
+        __syncthreads();                                         // LDS free for the next row
+    }
+}
+
+// ---- HBM kernel (class 3): two HBM tuple buffers per workgroup, messages in chunks -------
+
+template <bool kEv>
+__device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, uint64_t *base,
+                                           int64_t C, int32_t lr, uint32_t r, int32_t k, const int32_t *src,
+                                           const int32_t *slot, DMark &pm) {
+    const int32_t tid = threadIdx.x, V = a.view;
+    const uint32_t t5 = uint32_t(a.tick) & 31u, tr = uint32_t(a.tremove);
+    int32_t lgV = 0;
+    while ((1 << lgV) < V) ++lgV;
+    const int32_t Vp = 1 << lgV;
+    int64_t xo = 0;
+    int32_t L = d_own<kHT>(a, sh, base, lr, r);
+    pm.mark(1);
+    uint32_t merged = 0;
+    for (int32_t m0 = 0; m0 < k;) {                              // block-uniform chunks
+        const int32_t Lp = (L + Vp - 1) >> lgV << lgV;
+        // the most messages with Lp + kc Vp + the senders' runs <= C
+        int64_t kc = (C - Lp - Vp) / Vp;
+        if (kc > k - m0) kc = k - m0;
+        if (kc > kMaxChunk) kc = kMaxChunk;
+        while (kc > 0 && Lp + kc * Vp + (kc + Vp - 1) / Vp * Vp > C) --kc;
+        if (kc < 1) {                                            // the list fills the buffer
+            if (tid == 0) atomicCAS(a.err, 0, a.tick);
+            if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
+            return;
+        }
+        uint64_t *X = base + xo, *Y = base + (C - xo);
+        merged += d_build<kHT>(a, X, Y, L, Lp, m0, int32_t(kc), Vp, lgV, src, slot, r);
+        pm.mark(2);
+        const int32_t N = Lp + (int32_t(kc) << lgV) + ((int32_t(kc) + Vp - 1) >> lgV << lgV);
+        xo = d_merge_runs(base, C, xo, N, Vp);
+        pm.mark(3);
+        L = d_fold(sh, base + xo, base + (C - xo), N, t5, tr);
+        pm.mark(4);
+        m0 += int32_t(kc);
+    }
+    d_finish<kEv, kHT>(a, sh, base + xo, L, lr, r, k, merged, pm);
+}
+
+template <bool kEv>
+__device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, int32_t lr, uint64_t *scratch,
+                          int32_t it) {
+    const int32_t tid = threadIdx.x;
+    const uint32_t r = uint32_t(a.row0 + lr);
+    if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);       // tests: each row exactly once
+    // crashed, not started yet, or the job stopped
+    if (a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) || *a.err) {
+        if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
+        return;
+    }
     const int64_t cap = a.scratch_cap;
-    DrainList d{0, false, scratch, scratch + cap, scratch + 2 * cap, scratch + 3 * cap};
     const int32_t o0 = a.csr_off[lr];
     const int32_t k = a.csr_off[lr + 1] - o0;
     int32_t *src = a.csr_src + o0;
     int32_t *slot = a.csr_slot ? a.csr_slot + o0 : nullptr;
-    // 1. ascending sender order
+    DMark pm;
+    pm.init(a.prof, it, k);
+    // 1. ascending sender order (keys in LDS, or in the HBM buffers)
     int32_t P = 1;
     while (P < k) P <<= 1;
-    if (P <= a.drain_lds) {
-        d_sort_segment(src, slot, k, P, a.row0, reinterpret_cast<uint64_t *>(sh.ids));
-    } else if (P <= cap) {
-        d_sort_segment(src, slot, k, P, a.row0, reinterpret_cast<uint64_t *>(d.aid));
+    if (P <= kHKeys) {
+        d_sort_segment<kHT>(src, slot, k, P, a.row0, sh.buf);
+    } else if (P <= 2 * cap) {
+        d_sort_segment<kHT>(src, slot, k, P, a.row0, scratch);
     } else {
         if (tid == 0) atomicCAS(a.err, 0, a.tick);
         if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
         return;
     }
-    // 2. the own view, this node itself left out (never listed)
-    {
-        const uint64_t e = tid < V ? __builtin_nontemporal_load(a.prev + int64_t(lr) * V + tid) : kPvEmpty;
-        const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
-        const bool keep = e != kPvEmpty && x != r && v != 0u;
-        uint32_t tot = 0;
-        const uint32_t pos = d_scan(keep ? 1u : 0u, &tot, sh.red[1]);
-        if (keep) { sh.ids[pos] = x; sh.vals[pos] = v | kOwnBit; }
-        d.L = int32_t(tot);
-        __syncthreads();
-    }
-    // 3. every message, ascending sender; the next payload is loaded while one merges
-    // a JOINREP (join schedule without an introducer list: validated on the host) is node 0's
-    // sender entry with an empty payload
-    auto payload = [&](int32_t j) -> uint64_t {
-        if (src[j] == kJoinRepSrc) return kPvEmpty;
-        const int32_t sl = slot ? slot[j] : src[j] - a.row0;
-        const uint64_t *row = sl >= 0 ? a.prev + int64_t(sl) * V : a.remote + int64_t(-sl - 1) * V;
-        return tid < V ? __builtin_nontemporal_load(row + tid) : kPvEmpty;
-    };
-    uint32_t merged = 0;
-    uint64_t nxt = k > 0 ? payload(0) : kPvEmpty;
-    for (int32_t j = 0; j < k; ++j) {
-        const uint64_t e = nxt;
-        const int32_t sj = __builtin_amdgcn_readfirstlane(src[j]);
-        const uint32_t s = sj == kJoinRepSrc ? 0u : uint32_t(sj);
-        if (j + 1 < k) nxt = payload(j + 1);
-        merged += e != kPvEmpty ? 1u : 0u;
-        if (!d.hbm && d.L + V + 1 > a.drain_lds) {              // spill the list to HBM
-            for (int32_t i = tid; i < d.L; i += kDT) { d.aid[i] = sh.ids[i]; d.aval[i] = sh.vals[i]; }
-            d.hbm = true;
-            __syncthreads();
-        }
-        if (d.hbm) {
-            if (d.L + V + 1 > cap) {                             // past the scratch: stop the job
-                if (tid == 0) atomicCAS(a.err, 0, a.tick);
-                if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
-                return;
-            }
-            d_message<true>(sh, d, r, s, e, t5, tr);
-        } else {
-            d_message<false>(sh, d, r, s, e, t5, tr);
-        }
-    }
-    // 4-5.
-    d_finish<kEv>(a, sh, d, lr, r, k, merged);
+    pm.mark(0);
+    d_body_hbm<kEv>(a, sh, scratch, cap, lr, r, k, src, slot, pm);
 }
 
-// Persistent: each workgroup takes the listed rows blockIdx.x, blockIdx.x + grid, ...
 template <bool kEv>
-__global__ void __launch_bounds__(kDT, 2) pview_drain_kernel(PviewTickArgs a) {
-    __shared__ DrainShared sh;
-    const int32_t cnt = a.long_list[0];
-    uint32_t *scratch = a.scratch + int64_t(blockIdx.x) * 4 * a.scratch_cap;
+__global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a) {
+    __shared__ DrainShared<kHT, kHKeys> sh;
+    const int32_t cnt = a.long_list[3];
+    const int32_t *list = a.long_list + 4 + 3 * int64_t(a.rows);
+    uint64_t *scratch = reinterpret_cast<uint64_t *>(a.scratch) + int64_t(blockIdx.x) * 2 * a.scratch_cap;
     for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
-        d_row<kEv>(a, sh, a.long_list[1 + i], scratch);
+        d_row_hbm<kEv>(a, sh, list[i], scratch, (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
         __syncthreads();                                         // LDS free for the next row
     }
+}
+
+template <bool kEv>
+void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
+    const unsigned cus = unsigned(a.cus);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 256, 4096, 0>), dim3(4 * cus), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 512, 8192, 1>), dim3(2 * cus), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 1024, kDrainLdsMax, 2>), dim3(cus), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(cus), dim3(kHT), 0, st, a);
 }
 
 }  // namespace
 
 hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st) {
     if (!a.drain || a.rows == 0) return hipSuccess;
-    if (!a.long_list || !a.scratch || a.drain_grid < 1 || a.scratch_cap < kDrainCap ||
-        a.drain_lds < 1 || a.drain_lds > kDrainCap)
+    if (!a.long_list || !a.scratch || a.cus < 1 || a.scratch_cap < 8192 || a.drain_lds < 1 ||
+        a.drain_lds > kDrainLdsMax)
         return hipErrorInvalidValue;
-    const dim3 g(unsigned(a.drain_grid)), blk(kDT);
-    if (a.ev.buf) hipLaunchKernelGGL(pview_drain_kernel<true>, g, blk, 0, st, a);
-    else hipLaunchKernelGGL(pview_drain_kernel<false>, g, blk, 0, st, a);
+    if (a.ev.buf) launch_drain_classes<true>(a, st);
+    else launch_drain_classes<false>(a, st);
     return hipGetLastError();
 }
 

@@ -40,8 +40,8 @@ struct PvShard {
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, out_pos, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok,
         rows_run,                // tests (GSP_TEST_PV_COUNT_ROWS=1): rows run per tick
-        long_list;               // drain-all: [1 + rows] the rows sent > kPvMaxInbox messages
-    gsp::DevBuf<uint32_t> scratch;     // drain-all: the drain kernel's HBM lists
+        long_list;               // drain-all: [4 + 4 rows] the rows sent > kPvMaxInbox messages, by class
+    gsp::DevBuf<uint32_t> scratch;     // drain-all: the HBM drain kernel's tuple buffers
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
     gsp::EvRing ev;
@@ -87,9 +87,9 @@ struct gsp_pview {
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
-    int32_t drain_grid = 0;      // drain kernel workgroups: 2 per CU (64 KB of LDS each)
-    int64_t scratch_cap = 0;     // drain kernel: entries per HBM list
-    int32_t drain_lds = 8192;    // drain kernel: LDS list capacity (GSP_TEST_PV_DRAIN_LDS lowers it)
+    int64_t scratch_cap = 0;     // HBM drain kernel: tuples per buffer (two per workgroup)
+    int32_t drain_lds = gsp::kDrainLdsMax;   // drain kernels: LDS tuples (GSP_TEST_PV_DRAIN_LDS lowers it)
+    int32_t drain_wide = 0;      // tests: GSP_TEST_PV_DRAIN_WIDE=w runs the rows of classes < w in class w
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail, h_start;
@@ -165,8 +165,9 @@ struct gsp_pview {
             a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
             a.scratch = sh.scratch.p;
             a.scratch_cap = scratch_cap;
-            a.drain_grid = drain_grid;
+            a.cus = cus;
             a.drain_lds = drain_lds;
+            a.drain_wide = drain_wide;
         }
         return a;
     }
@@ -189,6 +190,9 @@ struct gsp_pview {
         a.err = local[0].err.p;
         a.drain = drain ? 1 : 0;
         a.long_list = drain ? sh.long_list.p : nullptr;
+        a.view = p.view;
+        a.drain_lds = drain_lds;
+        a.drain_wide = drain_wide;
         return a;
     }
 
@@ -279,9 +283,9 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     }
     if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
     if (s->drain) {
-        GSP_HIP(sh.long_list.alloc(rows + 1));
-        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 4, st));
-        GSP_HIP(sh.scratch.alloc(size_t(s->drain_grid) * 4 * size_t(s->scratch_cap)));
+        GSP_HIP(sh.long_list.alloc(4 + size_t(gsp::kDrainClasses) * rows));
+        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 16, st));
+        GSP_HIP(sh.scratch.alloc(size_t(s->cus) * 4 * size_t(s->scratch_cap)));   // 2 x u64 per CU
     }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
@@ -290,8 +294,8 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
         GSP_HIP(hipMemsetAsync(sh.rows_run.p, 0, size_t(s->p.max_ticks + 1) * 4, st));
     }
     if (const char *pf = std::getenv("GSP_PV_PROFILE"); pf && std::atoi(pf)) {
-        GSP_HIP(sh.prof.alloc(64 * 8 * gsp::kPvProfPhases));
-        GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * 8 * gsp::kPvProfPhases * 8, st));
+        GSP_HIP(sh.prof.alloc(64 * 16 * gsp::kPvProfPhases));   // k slots 8-15: the drain kernel
+        GSP_HIP(hipMemsetAsync(sh.prof.p, 0, 64 * 16 * gsp::kPvProfPhases * 8, st));
     }
     GSP_HIP(hipMemsetAsync(sh.dig.p, 0, dig * 8, st));
     GSP_HIP(hipMemsetAsync(sh.own_hb.p, 0, rows * 4, st));
@@ -433,14 +437,16 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
     s->drain = p->inbox == 0;
     if (s->drain) {
-        // two 64 KB-LDS workgroups per CU; each holds an HBM list pair for the rows whose list
-        // outgrows LDS: a power of two >= n (a list holds distinct ids, a segment distinct
-        // senders), at most 2^19 entries (the job stops past it, GSP_ERR_CAPACITY)
-        s->drain_grid = 2 * s->cus;
+        // the HBM drain kernel (class 3 rows) runs one 1024-lane workgroup per CU, each with two
+        // HBM tuple buffers: a power of two >= n + 3 kPvMaxView (a list of distinct ids plus one
+        // message's runs always fits, so any row finishes in chunks), at most 2^19 tuples (a
+        // list past it stops the job, GSP_ERR_CAPACITY)
         s->scratch_cap = 8192;
-        while (s->scratch_cap < p->n && s->scratch_cap < (int64_t(1) << 19)) s->scratch_cap <<= 1;
+        while (s->scratch_cap < int64_t(p->n) + 3 * gsp::kPvMaxView && s->scratch_cap < (int64_t(1) << 19))
+            s->scratch_cap <<= 1;
         if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
-            s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(8192, std::atoi(dl)));
+            s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(gsp::kDrainLdsMax, std::atoi(dl)));
+        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(2, std::atoi(dw)));
     }
     s->pos_scatter = !s->rowmode && !s->joins;
     if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
@@ -525,11 +531,13 @@ int gsp_pview_destroy(gsp_pview *s) {
     for (PvShard &sh : s->local) {
         if (sh.prof.p) {   // GSP_PV_PROFILE diagnostics: cycles per phase of sampled rows, by k
             constexpr int P = gsp::kPvProfPhases;
-            std::vector<unsigned long long> h(64 * 8 * P);
+            std::vector<unsigned long long> h(64 * 16 * P);
             if (hipMemcpy(h.data(), sh.prof.p, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-                unsigned long long ph[8][P] = {{0}};
-                for (size_t i = 0; i < h.size(); ++i) ph[(i / P) % 8][i % P] += h[i];
-                for (int k = 0; k < 8; ++k) {
+                unsigned long long ph[16][P] = {{0}};
+                for (size_t i = 0; i < h.size(); ++i) ph[(i / P) % 16][i % P] += h[i];
+                // k 0-7: the tick kernels; 8-15: the drain kernel's rows, k in [8 (b - 7), 8 (b - 6))
+                // (15: k >= 64)
+                for (int k = 0; k < 16; ++k) {
                     const unsigned long long rows = ph[k][P - 1];
                     if (!rows) continue;
                     unsigned long long tot = 0;
@@ -590,7 +598,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         if (int rc = pv_join_scatter(s, t)) return rc;
         for (PvShard &sh : s->local) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
-            if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 4, s->st));
+            if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 16, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
         }
         // ranks: the receipt kernels' capacity flags, MAX over the ranks before any tick kernel

@@ -220,7 +220,7 @@ struct PvMark {
     uint64_t last = 0;
     __device__ __forceinline__ void init(unsigned long long *prof, int32_t k) {
         if (prof && threadIdx.x == 0 && (blockIdx.x & 15u) == 0) {
-            out = prof + ((blockIdx.x >> 4 & 63u) * 8 + uint32_t(k & 7)) * kPvProfPhases;
+            out = prof + ((blockIdx.x >> 4 & 63u) * 16 + uint32_t(k & 7)) * kPvProfPhases;
             atomicAdd(out + kPvProfPhases - 1, 1ull);
             last = clock64();
         }
@@ -1105,14 +1105,18 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
         else pv_best8_scan(a, o0, 0, k_all, 1, bs, bl);
         k = (k_all > a.max_segment || lng) ? 0 : (k_all < a.inbox ? k_all : a.inbox);
     }
-    if (a.drain) {           // the long rows of this wave: one atomic per wave
-        const unsigned long long lm = __ballot(lng);
-        if (lm) {
-            const int32_t lane0 = __builtin_ffsll(lm) - 1;
-            int32_t base = 0;
-            if (lane == lane0) base = atomicAdd(&a.long_list[0], __popcll(lm));
-            base = __shfl(base, lane0, 64);
-            if (lng) a.long_list[1 + base + __popcll(lm & ((1ull << lane) - 1ull))] = lr;
+    if (a.drain) {           // the long rows of this wave by drain class: one atomic per class
+        const int32_t c = lng ? pv_drain_class(k_all, a.view, a.drain_lds, a.drain_wide) : -1;
+#pragma unroll
+        for (int q = 0; q < kDrainClasses; ++q) {
+            const unsigned long long lm = __ballot(c == q);
+            if (lm) {
+                const int32_t lane0 = __builtin_ffsll(lm) - 1;
+                int32_t base = 0;
+                if (lane == lane0) base = atomicAdd(&a.long_list[q], __popcll(lm));
+                base = __shfl(base, lane0, 64);
+                if (c == q) a.long_list[4 + q * a.rows + base + __popcll(lm & ((1ull << lane) - 1ull))] = lr;
+            }
         }
     }
     // the wave's wide rows, one after the other (wave-uniform loop)

@@ -72,15 +72,35 @@ struct PviewTickArgs {
     // drain-all (gsp_pview_params.inbox = 0, pview_drain.hip): a row sent more than
     // kPvMaxInbox messages is listed by the receipt kernel and merges them all there
     int32_t drain;               // 1: inbox 0 (the tick kernels skip the listed rows)
-    const int32_t *long_list;    // [1 + rows]: count, then the listed rows
+    const int32_t *long_list;    // [4 + kDrainClasses * rows]: counts, then the rows per class
     const int32_t *csr_off;      // [rows + 1] this tick's receiver CSR
     int32_t *csr_src, *csr_slot; // its senders (sorted in place) and rows (row mode, or null)
-    uint32_t *scratch;           // [drain_grid][4][scratch_cap]: HBM lists of long rows
-    int64_t scratch_cap;         // entries per list (>= the LDS capacity, a power of two)
-    int32_t drain_grid;          // drain kernel workgroups (persistent)
-    int32_t drain_lds;           // LDS list / segment-sort capacity in use (tests lower it to
-                                 // reach the HBM paths, GSP_TEST_PV_DRAIN_LDS), <= 8192
+    uint32_t *scratch;           // [cus][2][scratch_cap] u64: HBM tuple buffers (class 3 rows)
+    int64_t scratch_cap;         // tuples per buffer (>= 8192, a power of two)
+    int32_t cus;                 // compute units: the drain kernels' persistent grids
+    int32_t drain_lds;           // LDS tuple capacity in use (tests lower it to reach the HBM
+                                 // kernel, GSP_TEST_PV_DRAIN_LDS), <= kDrainLdsMax
+    int32_t drain_wide;          // tests (GSP_TEST_PV_DRAIN_WIDE=w): the rows of classes < w run
+                                 // in class w
 };
+
+// Drain-all row classes (pview_drain.hip), by the row's update tuples: own view + k payloads
+// (Vp = pow2(V) slots each) + the senders' runs.  In LDS (k <= kDrainStage): 0: <= 4,096
+// tuples, 256-lane rows, 4 per CU; 1: <= 8,192, 512-lane rows, 2 per CU; 2: <= 16,384,
+// 1024-lane rows, 1 per CU.  3: the rest, 1024-lane rows in HBM buffers (and every row of a
+// view below 8 slots).
+constexpr int kDrainClasses = 4;
+constexpr int kDrainStage = 64;
+constexpr int kDrainLdsMax = 16384;
+__host__ __device__ inline int32_t pv_drain_class(int32_t k, int32_t view, int32_t lds, int32_t wide) {
+    int32_t vp = 1;
+    while (vp < view) vp <<= 1;
+    const int64_t need = int64_t(vp) * (1 + k) + (int64_t(k) + vp - 1) / vp * vp;
+    if (vp < 8 || k > kDrainStage || need > lds) return 3;
+    if (wide < 1 && need <= 4096) return 0;
+    if (wide < 2 && need <= 8192) return 1;
+    return need <= kDrainLdsMax ? 2 : 3;
+}
 constexpr int kPvProfPhases = 16;   // per (slot, k): phases 0..14, rows sampled
 
 struct PviewReceiptArgs {
@@ -92,7 +112,8 @@ struct PviewReceiptArgs {
     int32_t *kcount, *order;     // k-bucketed row order for the tick kernel (or null)
     int32_t *err;
     int32_t drain;               // inbox 0: rows sent more than kPvMaxInbox messages go to
-    int32_t *long_list;          // long_list ([1 + rows], count first), not into the buckets
+    int32_t *long_list;          // long_list (by pv_drain_class), not into the buckets
+    int32_t view, drain_lds, drain_wide;
 };
 
 hipError_t launch_pview_init(const PviewTickArgs &a, hipStream_t st);

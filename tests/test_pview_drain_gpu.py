@@ -6,8 +6,9 @@ run in pview_drain_kernel (gossip_protocol_amd/csrc/pview_drain.hip), which merg
 ascending sender order.  Every tick's digest (no overflow), the message lists and the views must
 equal the oracle's, which folds every message of every row the same way.  The cases make most
 rows long (fan-out 8 and 16 against small views), make hubs past 1,000 senders (a join burst
-of 2,000 nodes knowing only the introducer), and force the drain kernel's HBM paths (a list or
-segment past its LDS capacity, GSP_TEST_PV_DRAIN_LDS lowers it).
+of 2,000 nodes knowing only the introducer), and force the drain kernel's HBM paths (a row's
+update tuples or segment past its LDS capacity, GSP_TEST_PV_DRAIN_LDS lowers it; the hubs also
+take their messages in several chunks, the list carried between them).
 """
 import numpy as np
 import pytest
@@ -80,8 +81,20 @@ CASES = [
 ]
 
 
+# the drain kernels' row classes (pv_drain_class): "lds" as sized (class 0: <= 4,096 tuples,
+# 256 lanes), "wide" / "wide2" (GSP_TEST_PV_DRAIN_WIDE=1 / 2: those rows as class 1, 512 lanes,
+# or class 2, 1024 lanes), "hbm" (GSP_TEST_PV_DRAIN_LDS=300: every long row in the HBM kernel)
+def _set_class(monkeypatch, cls):
+    if cls in ("wide", "wide2"):
+        monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", "1" if cls == "wide" else "2")
+    elif cls == "hbm":
+        monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
+
+
+@pytest.mark.parametrize("cls", ["lds", "wide", "wide2"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d" % c[:3])
-def test_drain_all_matches_oracle(case):
+def test_drain_all_matches_oracle(case, cls, monkeypatch):
+    _set_class(monkeypatch, cls)
     n, V, f, drop, mode, ftick, ppm, seed, ticks = case
     kw = dict(view=V, fanout=f, inbox=0, drop_pct=drop, fail_mode=mode, fail_tick=ftick,
               fail_ppm=ppm, seed=seed)
@@ -89,10 +102,12 @@ def test_drain_all_matches_oracle(case):
     assert longest > 7
 
 
+@pytest.mark.parametrize("cls", ["lds", "wide", "wide2", "hbm"])
 @pytest.mark.parametrize("evict_order", [0, 1])
-def test_drain_all_events_and_rows_run(monkeypatch, evict_order):
+def test_drain_all_events_and_rows_run(monkeypatch, evict_order, cls):
     """Every join / remove / evict record of the long rows, every row run exactly once (the
-    split kernels skip the long rows; the drain kernel runs them)."""
+    split kernels skip the long rows; the drain kernels run them), in every row class."""
+    _set_class(monkeypatch, cls)
     monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=30000,
               seed=17, tremove=10, evict_order=evict_order)
@@ -112,9 +127,9 @@ def test_drain_all_kernel_forms(monkeypatch, form):
 
 
 def test_drain_all_hbm_paths(monkeypatch):
-    """GSP_TEST_PV_DRAIN_LDS=300: a long row's list moves to the workgroup's HBM scratch once it
-    could pass 300 entries, and a segment of more than 256 senders is sorted in HBM."""
-    monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
+    """GSP_TEST_PV_DRAIN_LDS=300: every long row's update tuples (more than 300) are sorted and
+    folded in the HBM kernel's buffers instead of LDS."""
+    _set_class(monkeypatch, "hbm")
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=5, fail_ppm=20000, seed=31)
     _run(3000, 16, kw, every=4)
 
@@ -122,8 +137,9 @@ def test_drain_all_hbm_paths(monkeypatch):
 def test_drain_all_join_burst_past_1000_senders(monkeypatch):
     """2,000 nodes start in one tick knowing only the introducer (no introducer list) and all
     gossip to it: node 0 is sent more than 1,000 messages a tick and merges every one of them
-    (the inbox-7 engine drops all but 7); with a low LDS bound its list and its segment sort
-    also take the HBM paths."""
+    (the inbox-7 engine drops all but 7).  Its tuples pass the HBM buffers (8,192 tuples at
+    n = 5,000), so it merges them in chunks of messages with its list carried between chunks;
+    with a low LDS bound its segment sort takes the HBM path too."""
     kw = dict(view=64, fanout=3, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=20000,
               seed=43)
     pol = dict(step_rate=0.0005, intro_list=0)
