@@ -53,7 +53,7 @@ namespace gsp {
 namespace {
 
 constexpr int kHT = 1024;                       // threads per HBM-kernel workgroup (16 waves)
-constexpr int kHKeys = 2048;                    // HBM kernel: LDS keys for the segment sort
+constexpr int kHBlock = 16384;                  // HBM kernel: tuples sorted per LDS block
 constexpr uint64_t kNone = ~0ull;               // an empty tuple: sorts last
 constexpr uint32_t kNoId = 0xFFFFFFFFu;
 constexpr int32_t kMaxChunk = 32767;            // messages per chunk: m is 15 bits
@@ -244,13 +244,13 @@ __device__ __forceinline__ uint32_t d_build(const PviewTickArgs &a, P X, uint64_
     return merged;
 }
 
-// Chunk step 3 (HBM kernel): merge-path merges of the sorted runs of width Vp, X <-> Y;
+// Chunk step 3 (HBM kernel): merge-path merges of the sorted runs of width w0, X <-> Y;
 // returns the offset of the sorted buffer.
-__device__ __forceinline__ int64_t d_merge_runs(uint64_t *base, int64_t C, int64_t xo, int32_t N, int32_t Vp) {
+__device__ __forceinline__ int64_t d_merge_runs(uint64_t *base, int64_t C, int64_t xo, int32_t N, int32_t w0) {
     const int32_t tid = threadIdx.x;
     int32_t E = 2;                                               // outputs per lane and pass
     while (E < 16 && int64_t(E) * kHT < N) E <<= 1;
-    for (int32_t w = Vp; w < N; w <<= 1) {
+    for (int32_t w = w0; w < N; w <<= 1) {
         const uint64_t *X = base + xo;
         uint64_t *Y = base + (C - xo);
         const int32_t Ew = E < 2 * w ? E : 2 * w;                // divides 2w: one pair per piece
@@ -614,29 +614,31 @@ __device__ __forceinline__ void d_merge_ip(P X, int32_t N, int32_t Vp) {
     }
 }
 
-// Each id's run folded in place.  Pass 1: lane t loads its F tuples into registers (one batch
-// of independent LDS reads), folds the runs that start among them in registers -- a run that
-// continues past them is walked on in LDS (rare) -- and writes each run's result over the
-// run's first tuple (id kept: a neighbour only reads a run head to see that its own run has
-// ended; results have m = 0, the runs' other tuples m >= 1).  Pass 2: after a barrier the lane
-// loads its results and, after the scan's barrier, writes them compacted in id order.
-// Returns the list length.
+// Each id's run folded in place, over the tuples S[sb, sb + n) of a sorted sequence of N.
+// Pass 1: lane t loads its F tuples into registers (one batch of independent reads), folds the
+// runs that start among them in registers -- a run that continues past them is walked on in
+// S (rare; it may cross into the next block) -- and writes each run's result over the run's
+// first tuple (id kept: a neighbour only reads a run head to see that its own run has ended;
+// results have m = 0, the runs' other tuples m >= 1).  Pass 2: after a barrier the lane loads
+// its results and, after the scan's barrier, writes them compacted in id order from S[out0].
+// prev0: the id of the tuple before the block (read before anything overwrote it).  Returns
+// the results written.
 template <int NT, int F, class Sh, class P>
-__device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5, uint32_t tr) {
-    const int32_t i0 = int32_t(threadIdx.x) * F;
+__device__ __forceinline__ int32_t d_fold_block(Sh &sh, P S, int32_t sb, int32_t n, int32_t N, uint32_t prev0,
+                                                int32_t out0, uint32_t t5, uint32_t tr) {
+    const int32_t i0 = sb + int32_t(threadIdx.x) * F, iend = sb + n;
     uint64_t tu[F];
 #pragma unroll
-    for (int q = 0; q < F; ++q) tu[q] = i0 + q < N ? S[i0 + q] : kNone;
-    const uint32_t prev = i0 > 0 && i0 < N ? uint32_t(S[i0 - 1] >> 32) : kNoId;
+    for (int q = 0; q < F; ++q) tu[q] = i0 + q < iend ? S[i0 + q] : kNone;
+    const uint32_t prev = threadIdx.x == 0 ? prev0 : i0 < iend ? uint32_t(S[i0 - 1] >> 32) : kNoId;
     uint32_t cnt = 0;
-    uint32_t rx = kNoId, cur = 0, own = 0;                       // the run being folded
+    uint32_t cur = 0, own = 0;                                   // the run being folded
     int32_t at0 = -1;                                            // its first tuple (this lane's)
 #pragma unroll
     for (int q = 0; q < F; ++q) {
         const uint32_t x = uint32_t(tu[q] >> 32);
         const uint32_t px = q == 0 ? prev : uint32_t(tu[q > 0 ? q - 1 : 0] >> 32);
         if (x != px) {                                           // a run starts here
-            rx = x;
             cur = 0;
             own = 0;
             at0 = x != kNoId ? q : -1;
@@ -651,12 +653,11 @@ __device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5
                 cur = pv_merge(cur, v, t5, tr);                  // MP1Node.cpp:247-251, 282-301
             }
         }
-        (void)rx;
+        const bool last = q + 1 == F || i0 + q + 1 == iend;     // this lane's last tuple
         const uint32_t nx = q + 1 < F ? uint32_t(tu[q + 1 < F ? q + 1 : q] >> 32) : kNoId;
-        const bool ends = q + 1 < F ? nx != x : true;
-        if (ends && at0 >= 0) {
-            if (q + 1 == F) {                                    // may continue past this lane
-                for (int32_t j = i0 + F; j < N; ++j) {
+        if (at0 >= 0 && (last || nx != x)) {
+            if (last) {                                          // may continue past this lane
+                for (int32_t j = i0 + q + 1; j < N; ++j) {
                     const uint64_t u = S[j];
                     if (uint32_t(u >> 32) != x) break;
                     const uint32_t lo = uint32_t(u), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
@@ -679,17 +680,23 @@ __device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5
 #pragma unroll
     for (int q = 0; q < F; ++q) {
         const int32_t i = i0 + q;
-        const uint64_t t = i < N ? S[i] : kNone;
+        const uint64_t t = i < iend ? S[i] : kNone;
         const uint32_t lo = uint32_t(t);
         res[q] = (t != kNone && (lo >> 17) == 0u && (lo & 0xFFFFu) != 0u) ? t : 0ull;
     }
-    uint32_t L = 0;
-    uint32_t at = d_scan<NT>(cnt, &L, sh.red[0]);                // every result loaded by now
+    uint32_t tot = 0;
+    uint32_t at = uint32_t(out0) + d_scan<NT>(cnt, &tot, sh.red[0]);   // every result loaded
 #pragma unroll
     for (int q = 0; q < F; ++q)
-        if (res[q]) S[at++] = res[q];
+        if (res[q]) S[int32_t(at++)] = res[q];
     __syncthreads();
-    return int32_t(L);
+    return int32_t(tot);
+}
+
+// The fold of an LDS row: one block.  Returns the list length.
+template <int NT, int F, class Sh, class P>
+__device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5, uint32_t tr) {
+    return d_fold_block<NT, F>(sh, S, 0, N, N, kNoId, 0, t5, tr);
 }
 
 // One row of an LDS class, every message in one pass.
@@ -747,7 +754,7 @@ __global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a)
 // ---- HBM kernel (class 3): two HBM tuple buffers per workgroup, messages in chunks -------
 
 template <bool kEv>
-__device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, uint64_t *base,
+__device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<kHT, kHBlock> &sh, uint64_t *base,
                                            int64_t C, int32_t lr, uint32_t r, int32_t k, const int32_t *src,
                                            const int32_t *slot, DMark &pm) {
     const int32_t tid = threadIdx.x, V = a.view;
@@ -775,9 +782,35 @@ __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<k
         merged += d_build<kHT>(a, X, Y, L, Lp, m0, int32_t(kc), Vp, lgV, src, slot, r);
         pm.mark(2);
         const int32_t N = Lp + (int32_t(kc) << lgV) + ((int32_t(kc) + Vp - 1) >> lgV << lgV);
-        xo = d_merge_runs(base, C, xo, N, Vp);
+        // runs of Vp sorted into blocks of kHBlock in LDS (in-place merges: Vp >= 8), then the
+        // blocks merged in HBM
+        if (Vp >= 8) {
+            uint64_t *X2 = base + xo;
+            const SkewBuf B{sh.buf};
+            for (int32_t b0 = 0; b0 < N; b0 += kHBlock) {
+                const int32_t nb = N - b0 < kHBlock ? N - b0 : kHBlock;
+                for (int32_t i = tid; i < nb; i += kHT) B[i] = X2[b0 + i];
+                __syncthreads();
+                d_merge_ip<kHT, kHBlock / kHT>(B, nb, Vp);
+                for (int32_t i = tid; i < nb; i += kHT) X2[b0 + i] = B[i];
+                __syncthreads();
+            }
+        }
+        xo = d_merge_runs(base, C, xo, N, Vp >= 8 ? kHBlock : Vp);
         pm.mark(3);
-        L = d_fold(sh, base + xo, base + (C - xo), N, t5, tr);
+        {                                                        // fold, blocks of 8 K tuples
+            uint64_t *S2 = base + xo;
+            int32_t out = 0;
+            uint32_t carry = kNoId;
+            constexpr int kFB = kHT * 8;                         // 8 tuples per lane in HBM
+            for (int32_t b0 = 0; b0 < N; b0 += kFB) {
+                const int32_t nb = N - b0 < kFB ? N - b0 : kFB;
+                const uint32_t last_x = uint32_t(S2[b0 + nb - 1] >> 32);   // before any compaction
+                out += d_fold_block<kHT, 8>(sh, S2, b0, nb, N, carry, out, t5, tr);
+                carry = last_x;
+            }
+            L = out;
+        }
         pm.mark(4);
         m0 += int32_t(kc);
     }
@@ -785,7 +818,7 @@ __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<k
 }
 
 template <bool kEv>
-__device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, int32_t lr, uint64_t *scratch,
+__device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHBlock> &sh, int32_t lr, uint64_t *scratch,
                           int32_t it) {
     const int32_t tid = threadIdx.x;
     const uint32_t r = uint32_t(a.row0 + lr);
@@ -805,7 +838,7 @@ __device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, 
     // 1. ascending sender order (keys in LDS, or in the HBM buffers)
     int32_t P = 1;
     while (P < k) P <<= 1;
-    if (P <= kHKeys) {
+    if (P <= kHBlock) {
         d_sort_segment<kHT>(src, slot, k, P, a.row0, sh.buf);
     } else if (P <= 2 * cap) {
         d_sort_segment<kHT>(src, slot, k, P, a.row0, scratch);
@@ -820,7 +853,7 @@ __device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHKeys> &sh, 
 
 template <bool kEv>
 __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a) {
-    __shared__ DrainShared<kHT, kHKeys> sh;
+    __shared__ DrainShared<kHT, kHBlock> sh;
     const int32_t cnt = a.long_list[3];
     const int32_t *list = a.long_list + 4 + 3 * int64_t(a.rows);
     uint64_t *scratch = reinterpret_cast<uint64_t *>(a.scratch) + int64_t(blockIdx.x) * 2 * a.scratch_cap;
