@@ -490,14 +490,18 @@ __device__ __forceinline__ void pv_merge_row(const PviewTickArgs &a, Sh &sh, int
         // does the run end here?
         uint32_t nxt = e + 1 < Q ? ck[e + 1 < Q ? e + 1 : e] : next_key;
         if (e + 1 == Q && nxt != kKeyMax && key_id(nxt) == x) {   // continues into the next lane
-            int32_t pos = beg + Q;
-            while (pos < P) {
-                const uint32_t kk = C[pos];
-                if (kk == kKeyMax || key_id(kk) != x) break;
-                const uint32_t s2 = key_src(kk);
-                if (ajs && !adone && ajs < s2) { av = pv_event(av, t5); adone = true; }
-                av = pv_merge(av, sh.vals[s2 * kSlots + key_slot(kk)], t5, tr);
-                ++pos;
+            // a run holds at most one key per source: at most kJ more keys, a fixed trip count
+            bool go = true;
+#pragma unroll
+            for (int c2 = 0; c2 < kJ; ++c2) {
+                const int32_t pos = beg + Q + c2;
+                const uint32_t kk = (go && pos < P) ? C[pos < P ? pos : P - 1] : kKeyMax;
+                go = go && kk != kKeyMax && key_id(kk) == x;
+                if (go) {
+                    const uint32_t s2 = key_src(kk);
+                    if (ajs && !adone && ajs < s2) { av = pv_event(av, t5); adone = true; }
+                    av = pv_merge(av, sh.vals[s2 * kSlots + key_slot(kk)], t5, tr);
+                }
             }
             nxt = kKeyMax;
         }
