@@ -163,3 +163,34 @@ def test_snapshots_keep_send_time_lists():
         e.recv(2, [1])                                   # id 2 through the batched path
         e.process(2, [1], [exact.OP_LOOP], 0)
         assert e.member_list(1) == [(1, 1, 2)] + [x for x in sent_list if x[0] != 2]
+
+
+@pytest.mark.gpu
+def test_null_payload_push_keeps_the_version_alive():
+    """a detached GOSSIP handed back with a NULL payload (gsp_queue_push, payload =
+    the sender's version at send time) must count as in flight again.  Here id 3 takes its
+    messages and hands them back without lists while id 2's GOSSIP of the same version is still
+    queued, then the sender commits a newer list: both receivers must still merge the list the
+    GOSSIP was sent with (a double release of that version would make the second consumer fail
+    with GSP_ERR_ORDER)."""
+    from gossip_protocol_amd import exact
+    with _joined_engine() as e:
+        e.payload_snapshots(True)
+        e.recv(1, [0, 1, 2, 3])
+        e.process(1, [0], [exact.OP_LOOP], 0)            # introducer joins 2, 3, 4 and gossips
+        sent_list = e.member_list(0)
+        msgs = e.detach(2, 2)                            # id 3 takes its messages...
+        assert any(m[1] == 3 for m in msgs)
+        for src, typ, batch, _ in reversed(msgs):        # ...and hands them back, no lists
+            assert e.queue_push(2, src, typ, None, send_batch=batch) == 0
+        assert e.recv_callback(1, 0, 2, 3, [(3, 50, 1)]) == 0   # the sender commits a newer list
+        assert e.member_list(0) != sent_list
+        e.recv(2, [1])                                   # id 2: its own copy of the GOSSIP
+        e.process(2, [1, 2], [exact.OP_LOOP, exact.OP_LOOP], 0)
+        want = [(1, 1, 2)] + [x for x in sent_list if x[0] != 2]
+        assert e.member_list(1) == want
+        got3 = dict((x[0], x[1]) for x in e.member_list(2))
+        assert got3.get(1) == 1                          # the sender's entry, bumped at t = 2
+        for ident, hb, _ in sent_list:                   # the send-time list, not (3, 50)
+            if ident != 3:
+                assert got3.get(ident) == hb, (ident, got3)
