@@ -277,7 +277,9 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "xgmi_bytes_per_tick": xgmi, "xgmi_bytes_source": XGMI_SOURCE, "exchange_csr_ms": xch_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
-                     "kernel": "pview_tick_split_kernel (256- and 128-lane rows, per tick)",
+                     "kernel": ("pview_tick_split_kernel (256- and 128-lane rows, per tick)" if k_in else
+                                "pview_tick_split_kernel + pview_drain_{lds,hbm}_kernel (rows sent > 7 "
+                                "messages), per tick"),
                      "valu": _pview_valu(nodes, world, kern_ms, window) if headline else None,
                      "window_ticks": window,
                      "kernel_ms_per_tick": kern_ms, "algorithmic_bytes_per_tick": bytes_per_tick},
