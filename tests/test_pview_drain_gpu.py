@@ -149,6 +149,17 @@ def test_drain_all_join_burst_past_1000_senders(monkeypatch):
     assert _run(5000, 6, kw, policy=pol, every=3, check=range(0, 10)) > 1000
 
 
+def test_drain_all_hub_merges_blocks_in_hbm():
+    """n = 20,000: the HBM buffers hold 32,768 tuples, so node 0's chunks of a join burst pass
+    the 16,384-tuple LDS blocks -- each chunk's runs are sorted block by block in LDS and the
+    blocks merged in HBM, and the fold runs over several 8 K-tuple register blocks."""
+    kw = dict(view=64, fanout=3, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=20000,
+              seed=47)
+    pol = dict(step_rate=0.0005, intro_list=0)
+    longest = _run(20000, 6, kw, policy=pol, every=2, check=range(0, 12))
+    assert longest > 600, "node 0 must be sent more than 600 messages (got %d)" % longest
+
+
 def test_drain_all_row_shards():
     """Row shards (in-process group of 3): the long rows' senders come from other shards' rows
     (received views, csr_slot < 0)."""
