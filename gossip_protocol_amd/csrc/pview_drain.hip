@@ -280,52 +280,17 @@ __device__ __forceinline__ int64_t d_merge_runs(uint64_t *base, int64_t C, int64
     return xo;
 }
 
-// The fold of one id's run S[i, ...) (sorted tuples): the entry's value (0: absent) and
-// whether it was in the list before (own).
-template <class P>
-__device__ __forceinline__ uint32_t d_fold_run(const P &S, int32_t i, int32_t N, uint64_t t, uint32_t x,
-                                               uint32_t t5, uint32_t tr, uint32_t *own) {
-    uint32_t cur = 0, o = 0;
-    for (int32_t j = i; j < N; ++j) {                            // the id's run, in message order
-        const uint64_t u = j == i ? t : S[j];
-        if (uint32_t(u >> 32) != x) break;
-        const uint32_t lo = uint32_t(u), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
-        if (m == 0) {
-            if (v) { cur = v; o = fl; }
-        } else if (fl) {
-            cur = pv_event(cur, t5);                             // MP1Node.cpp:237-243
-        } else {
-            cur = pv_merge(cur, v, t5, tr);                      // MP1Node.cpp:247-251, 282-301
-        }
+// One tuple of an id's run applied to the run's state (cur: hb << 5 | ts5, 0 = absent; own:
+// the list flag of an m = 0 tuple), in message order.
+__device__ __forceinline__ void d_apply(uint32_t &cur, uint32_t &own, uint32_t lo, uint32_t t5, uint32_t tr) {
+    const uint32_t m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
+    if (m == 0) {
+        if (v) { cur = v; own = fl; }                            // the list (own view, earlier chunks)
+    } else if (fl) {
+        cur = pv_event(cur, t5);                                 // the sender: MP1Node.cpp:237-243
+    } else {
+        cur = pv_merge(cur, v, t5, tr);                          // a payload entry: :247-251, 282-301
     }
-    *own = o;
-    return cur;
-}
-
-// Chunk step 4 (HBM kernel): each id's run folded (sorted tuples S[0, N)); the new list,
-// compacted in id order, into S.  D: the other buffer.  Returns the list length.
-template <class Sh>
-__device__ __forceinline__ int32_t d_fold(Sh &sh, uint64_t *S, uint64_t *D, int32_t N, uint32_t t5,
-                                          uint32_t tr) {
-    const int32_t tid = threadIdx.x;
-    const int32_t F = (N + kHT - 1) / kHT, i0 = tid * F, i1 = i0 + F < N ? i0 + F : N;
-    uint32_t cnt = 0;
-    uint32_t prev = i0 > 0 && i0 < N ? uint32_t(S[i0 - 1] >> 32) : kNoId;
-    for (int32_t i = i0; i < i1; ++i) {
-        const uint64_t t = S[i];
-        const uint32_t x = uint32_t(t >> 32);
-        if (x == kNoId) break;                                   // the empty tuples: the tail
-        if (i > 0 && x == prev) continue;
-        prev = x;
-        uint32_t own;
-        const uint32_t cur = d_fold_run(S, i, N, t, x, t5, tr, &own);
-        if (cur) D[i0 + int32_t(cnt++)] = d_tuple(x, 0u, own, cur);
-    }
-    uint32_t L = 0;
-    const uint32_t at = d_scan<kHT>(cnt, &L, sh.red[0]);         // S read to its end by now
-    for (uint32_t q = 0; q < cnt; ++q) S[at + q] = D[i0 + int32_t(q)];
-    __syncthreads();
-    return int32_t(L);
 }
 
 // Step 5's bin selection (wave 0): the first bin where the running count reaches need;
@@ -643,16 +608,7 @@ __device__ __forceinline__ int32_t d_fold_block(Sh &sh, P S, int32_t sb, int32_t
             own = 0;
             at0 = x != kNoId ? q : -1;
         }
-        if (at0 >= 0) {                                          // a run of this lane
-            const uint32_t lo = uint32_t(tu[q]), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
-            if (m == 0) {
-                if (v) { cur = v; own = fl; }
-            } else if (fl) {
-                cur = pv_event(cur, t5);                         // MP1Node.cpp:237-243
-            } else {
-                cur = pv_merge(cur, v, t5, tr);                  // MP1Node.cpp:247-251, 282-301
-            }
-        }
+        if (at0 >= 0) d_apply(cur, own, uint32_t(tu[q]), t5, tr);   // a run of this lane
         const bool last = q + 1 == F || i0 + q + 1 == iend;     // this lane's last tuple
         const uint32_t nx = q + 1 < F ? uint32_t(tu[q + 1 < F ? q + 1 : q] >> 32) : kNoId;
         if (at0 >= 0 && (last || nx != x)) {
@@ -660,14 +616,7 @@ __device__ __forceinline__ int32_t d_fold_block(Sh &sh, P S, int32_t sb, int32_t
                 for (int32_t j = i0 + q + 1; j < N; ++j) {
                     const uint64_t u = S[j];
                     if (uint32_t(u >> 32) != x) break;
-                    const uint32_t lo = uint32_t(u), m = lo >> 17, fl = (lo >> 16) & 1u, v = lo & 0xFFFFu;
-                    if (m == 0) {
-                        if (v) { cur = v; own = fl; }
-                    } else if (fl) {
-                        cur = pv_event(cur, t5);
-                    } else {
-                        cur = pv_merge(cur, v, t5, tr);
-                    }
+                    d_apply(cur, own, uint32_t(u), t5, tr);
                 }
             }
             S[i0 + at0] = d_tuple(x, 0u, cur ? own : 0u, cur);   // cur = 0: absent
