@@ -153,6 +153,29 @@ __device__ void d_sort_segment(int32_t *src, int32_t *slot, int32_t k, int32_t P
     __syncthreads();
 }
 
+// The same for a short segment (k <= NT, the LDS classes): each lane ranks its key against all
+// k (distinct keys, broadcast LDS reads) and writes it at its rank -- two barriers instead of
+// the bitonic network's log^2 steps.
+template <int NT>
+__device__ void d_rank_segment(int32_t *src, int32_t *slot, int32_t k, int32_t row0, uint64_t *keys) {
+    const int32_t t = threadIdx.x;
+    uint64_t key = ~0ull;
+    if (t < k) {
+        const int32_t s = src[t];
+        const int32_t sl = slot ? slot[t] : s - row0;
+        key = (uint64_t(uint32_t(s + 1)) << 32) | uint64_t(uint32_t(sl));
+        keys[t] = key;
+    }
+    __syncthreads();
+    if (t < k) {
+        int32_t rank = 0;
+        for (int32_t j = 0; j < k; ++j) rank += keys[j] < key ? 1 : 0;
+        src[rank] = int32_t(uint32_t(key >> 32)) - 1;
+        if (slot) slot[rank] = int32_t(uint32_t(key));
+    }
+    __syncthreads();
+}
+
 // Diagnostics (GSP_PV_PROFILE=1): thread 0 adds the cycles of each phase of every 16th row a
 // workgroup runs to prof[slot][8 + min(7, (k - 8) / 8)][phase] (pview_engine.cpp prints them).
 struct DMark {
@@ -668,9 +691,7 @@ __device__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, int3
     int32_t *slot = a.csr_slot ? a.csr_slot + o0 : nullptr;
     DMark pm;
     pm.init(a.prof, it, k);
-    int32_t P = 1;
-    while (P < k) P <<= 1;
-    d_sort_segment<NT>(src, slot, k, P, a.row0, sh.buf);         // 1. ascending senders
+    d_rank_segment<NT>(src, slot, k, a.row0, sh.buf);            // 1. ascending senders
     pm.mark(0);
     int32_t lgV = 0;
     while ((1 << lgV) < V) ++lgV;
