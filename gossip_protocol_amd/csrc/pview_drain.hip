@@ -31,9 +31,10 @@
 //      order already, so a rotation is an offset into it;
 //   6. the new view in id order, the row's counts straight into the tick digest (a long
 //      row's counts overflow the per-row record's 8- and 16-bit fields), its events.
-// Row classes (pview_kernels.hpp pv_drain_class): rows of at most 4,096 / 8,192 / 16,384
-// tuples (k <= 14 / 30 / 62 at V = 256) run in LDS, one buffer merged and folded in place,
-// 256 / 512 / 1024 lanes per row and 4 / 2 / 1 rows per CU (pview_drain_lds_kernel); the
+// Row classes (pview_kernels.hpp pv_drain_class): rows of at most 3,072 / 4,096 / 8,192 /
+// 16,384 tuples (k <= 10 / 14 / 30 / 62 at V = 256) run in LDS, one buffer merged and folded
+// in place, 192 / 256 / 512 / 1024 lanes per row and 5 / 4 / 2 / 1 rows per CU
+// (pview_drain_lds_kernel); the
 // rest run in two HBM buffers per workgroup (pview_drain_hbm_kernel), the messages taken in
 // chunks when they do not fit at once, the list carried between chunks as the m = 0 run.  A
 // list past the HBM buffers stops the job (GSP_ERR_CAPACITY).
@@ -390,7 +391,7 @@ __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, in
     uint32_t T16 = 0x10000u, need2 = 0;
     if (int32_t(C) > V) {
         for (int pass = 0; pass < 2; ++pass) {
-            if (tid < 256) sh.hist[tid] = 0;
+            for (int32_t i = tid; i < 256; i += NT) sh.hist[i] = 0;
             __syncthreads();
             const uint32_t hi = pass ? T16 : 0u;
             for (int32_t i = tid; i < L; i += NT) {
@@ -535,12 +536,22 @@ __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, in
 template <int NT, class Sh, class P>
 __device__ __forceinline__ int32_t d_own(const PviewTickArgs &a, Sh &sh, P X, int32_t lr, uint32_t r) {
     const int32_t tid = threadIdx.x, V = a.view;
-    const uint64_t e = tid < V ? a.prev[int64_t(lr) * V + tid] : kPvEmpty;
-    const uint32_t x = uint32_t(e >> 32), v = uint32_t(e) & 0xFFFFu;
-    const bool keep = e != kPvEmpty && x != r && v != 0u;
+    const int32_t per = V > NT ? 2 : 1;                          // V <= 256 <= 2 NT: contiguous slots
+    uint64_t e[2];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int32_t i = tid * per + q;
+        e[q] = q < per && i < V ? a.prev[int64_t(lr) * V + i] : kPvEmpty;
+        const uint32_t x = uint32_t(e[q] >> 32), v = uint32_t(e[q]) & 0xFFFFu;
+        if (!(e[q] != kPvEmpty && x != r && v != 0u)) e[q] = kPvEmpty;
+        cnt += e[q] != kPvEmpty ? 1u : 0u;
+    }
     uint32_t tot = 0;
-    const uint32_t pos = d_scan<NT>(keep ? 1u : 0u, &tot, sh.red[1]);
-    if (keep) X[pos] = d_tuple(x, 0u, 1u, v);
+    uint32_t pos = d_scan<NT>(cnt, &tot, sh.red[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (e[q] != kPvEmpty) X[pos++] = d_tuple(uint32_t(e[q] >> 32), 0u, 1u, uint32_t(e[q]) & 0xFFFFu);
     __syncthreads();
     return int32_t(tot);
 }
@@ -714,14 +725,14 @@ template <bool kEv, int NT, int CAP, int kCls>
 __global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a) {
     __shared__ DrainShared<NT, CAP> sh;
     const int32_t cnt = a.long_list[kCls];
-    const int32_t *list = a.long_list + 4 + int64_t(kCls) * a.rows;
+    const int32_t *list = a.long_list + kDrainHead + int64_t(kCls) * a.rows;
     for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
         d_row_lds<kEv, NT, CAP>(a, sh, list[i], (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
         __syncthreads();                                         // LDS free for the next row
     }
 }
 
-// ---- HBM kernel (class 3): two HBM tuple buffers per workgroup, messages in chunks -------
+// ---- HBM kernel (class 4): two HBM tuple buffers per workgroup, messages in chunks -------
 
 template <bool kEv>
 __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<kHT, kHBlock> &sh, uint64_t *base,
@@ -824,8 +835,8 @@ __device__ void d_row_hbm(const PviewTickArgs &a, DrainShared<kHT, kHBlock> &sh,
 template <bool kEv>
 __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a) {
     __shared__ DrainShared<kHT, kHBlock> sh;
-    const int32_t cnt = a.long_list[3];
-    const int32_t *list = a.long_list + 4 + 3 * int64_t(a.rows);
+    const int32_t cnt = a.long_list[4];
+    const int32_t *list = a.long_list + kDrainHead + 4 * int64_t(a.rows);
     uint64_t *scratch = reinterpret_cast<uint64_t *>(a.scratch) + int64_t(blockIdx.x) * 2 * a.scratch_cap;
     for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
         d_row_hbm<kEv>(a, sh, list[i], scratch, (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
@@ -836,9 +847,10 @@ __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a
 template <bool kEv>
 void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
     const unsigned cus = unsigned(a.cus);
-    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 256, 4096, 0>), dim3(4 * cus), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 512, 8192, 1>), dim3(2 * cus), dim3(512), 0, st, a);
-    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 1024, kDrainLdsMax, 2>), dim3(cus), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 192, 3072, 0>), dim3(5 * cus), dim3(192), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 256, 4096, 1>), dim3(4 * cus), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 512, 8192, 2>), dim3(2 * cus), dim3(512), 0, st, a);
+    hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, 1024, kDrainLdsMax, 3>), dim3(cus), dim3(1024), 0, st, a);
     hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(cus), dim3(kHT), 0, st, a);
 }
 

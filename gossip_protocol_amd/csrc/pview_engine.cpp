@@ -40,7 +40,7 @@ struct PvShard {
     gsp::DevBuf<int32_t> len[2], own_hb, fail_tick, out_dst, out_pos, deg, off, fill, csr_src, err,
         tile_sum, rc_info, rc_src, rc_slot, kcount, order, start_tick, ping, joiners, join_ok,
         rows_run,                // tests (GSP_TEST_PV_COUNT_ROWS=1): rows run per tick
-        long_list;               // drain-all: [4 + 4 rows] the rows sent > kPvMaxInbox messages, by class
+        long_list;               // drain-all: the rows sent > kPvMaxInbox messages, by class
     gsp::DevBuf<uint32_t> scratch;     // drain-all: the HBM drain kernel's tuple buffers
     gsp::DevBuf<uint64_t> intro_buf;   // row layout, shards != 0: node 0's view of the last tick
     gsp::DevBuf<unsigned long long> dig, prof, rowdig;
@@ -283,8 +283,8 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     }
     if (s->p.events) GSP_HIP(sh.ev.alloc(s->p.events, s->p.event_cap, st));
     if (s->drain) {
-        GSP_HIP(sh.long_list.alloc(4 + size_t(gsp::kDrainClasses) * rows));
-        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 16, st));
+        GSP_HIP(sh.long_list.alloc(gsp::kDrainHead + size_t(gsp::kDrainClasses) * rows));
+        GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, gsp::kDrainHead * 4, st));
         GSP_HIP(sh.scratch.alloc(size_t(s->cus) * 4 * size_t(s->scratch_cap)));   // 2 x u64 per CU
     }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
@@ -437,7 +437,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
     s->drain = p->inbox == 0;
     if (s->drain) {
-        // the HBM drain kernel (class 3 rows) runs one 1024-lane workgroup per CU, each with two
+        // the HBM drain kernel (class 4 rows) runs one 1024-lane workgroup per CU, each with two
         // HBM tuple buffers: a power of two >= n + 3 kPvMaxView (a list of distinct ids plus one
         // message's runs always fits, so any row finishes in chunks), at most 2^19 tuples (a
         // list past it stops the job, GSP_ERR_CAPACITY)
@@ -446,7 +446,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
             s->scratch_cap <<= 1;
         if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
             s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(gsp::kDrainLdsMax, std::atoi(dl)));
-        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(2, std::atoi(dw)));
+        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(3, std::atoi(dw)));
     }
     s->pos_scatter = !s->rowmode && !s->joins;
     if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
@@ -598,7 +598,7 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         if (int rc = pv_join_scatter(s, t)) return rc;
         for (PvShard &sh : s->local) {
             if (s->sort_rows) GSP_HIP(hipMemsetAsync(sh.kcount.p, 0, 8 * 4, s->st));
-            if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, 16, s->st));
+            if (s->drain) GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, gsp::kDrainHead * 4, s->st));
             GSP_HIP(gsp::launch_pview_receipt(s->receipt(sh), s->st));
         }
         // ranks: the receipt kernels' capacity flags, MAX over the ranks before any tick kernel

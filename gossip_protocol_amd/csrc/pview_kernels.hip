@@ -1131,7 +1131,7 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
         if (c >= 0) {
             int32_t at = cls_base[c] + __popcll(mine & ((1ull << lane) - 1ull));
             for (int32_t w = 0; w < wave; ++w) at += cls_cnt[c][w];
-            a.long_list[4 + c * a.rows + at] = lr;
+            a.long_list[kDrainHead + c * a.rows + at] = lr;
         }
     }
     // the wave's wide rows, one after the other (wave-uniform loop)

@@ -72,7 +72,7 @@ struct PviewTickArgs {
     // drain-all (gsp_pview_params.inbox = 0, pview_drain.hip): a row sent more than
     // kPvMaxInbox messages is listed by the receipt kernel and merges them all there
     int32_t drain;               // 1: inbox 0 (the tick kernels skip the listed rows)
-    const int32_t *long_list;    // [4 + kDrainClasses * rows]: counts, then the rows per class
+    const int32_t *long_list;    // [kDrainHead + kDrainClasses * rows]: counts, then the rows per class
     const int32_t *csr_off;      // [rows + 1] this tick's receiver CSR
     int32_t *csr_src, *csr_slot; // its senders (sorted in place) and rows (row mode, or null)
     uint32_t *scratch;           // [cus][2][scratch_cap] u64: HBM tuple buffers (class 3 rows)
@@ -85,21 +85,24 @@ struct PviewTickArgs {
 };
 
 // Drain-all row classes (pview_drain.hip), by the row's update tuples: own view + k payloads
-// (Vp = pow2(V) slots each) + the senders' runs.  In LDS (k <= kDrainStage): 0: <= 4,096
-// tuples, 256-lane rows, 4 per CU; 1: <= 8,192, 512-lane rows, 2 per CU; 2: <= 16,384,
-// 1024-lane rows, 1 per CU.  3: the rest, 1024-lane rows in HBM buffers (and every row of a
-// view below 8 slots).
-constexpr int kDrainClasses = 4;
+// (Vp = pow2(V) slots each) + the senders' runs.  In LDS (k <= kDrainStage): 0: <= 3,072
+// tuples, 192-lane rows, 5 per CU; 1: <= 4,096, 256-lane rows, 4 per CU; 2: <= 8,192, 512-lane
+// rows, 2 per CU; 3: <= 16,384, 1024-lane rows, 1 per CU.  4: the rest, 1024-lane rows in HBM
+// buffers (and every row of a view below 8 slots).  long_list: kDrainHead counts, then the
+// rows of each class.
+constexpr int kDrainClasses = 5;
+constexpr int kDrainHead = 8;
 constexpr int kDrainStage = 64;
 constexpr int kDrainLdsMax = 16384;
 __host__ __device__ inline int32_t pv_drain_class(int32_t k, int32_t view, int32_t lds, int32_t wide) {
     int32_t vp = 1;
     while (vp < view) vp <<= 1;
     const int64_t need = int64_t(vp) * (1 + k) + (int64_t(k) + vp - 1) / vp * vp;
-    if (vp < 8 || k > kDrainStage || need > lds) return 3;
-    if (wide < 1 && need <= 4096) return 0;
-    if (wide < 2 && need <= 8192) return 1;
-    return need <= kDrainLdsMax ? 2 : 3;
+    if (vp < 8 || k > kDrainStage || need > lds) return 4;
+    if (wide < 1 && need <= 3072) return 0;
+    if (wide < 2 && need <= 4096) return 1;
+    if (wide < 3 && need <= 8192) return 2;
+    return need <= kDrainLdsMax ? 3 : 4;
 }
 constexpr int kPvProfPhases = 16;   // per (slot, k): phases 0..14, rows sampled
 

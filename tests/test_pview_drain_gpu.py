@@ -78,20 +78,23 @@ CASES = [
     (3000, 32, 8, 0, 1, 5, 20000, 3, 24),        # most rows sent > 7 messages
     (2000, 64, 3, 10, 2, 8, 50000, 7, 30),       # config-5 rules: a few long rows
     (4096, 16, 16, 10, 1, 6, 10000, 5, 16),      # full fan-out to a 16-entry view: k ~ 14
+    (3000, 256, 8, 10, 2, 5, 50000, 11, 10),     # config 5's view: 256 slots, more than 192 lanes
 ]
 
 
-# the drain kernels' row classes (pv_drain_class): "lds" as sized (class 0: <= 4,096 tuples,
-# 256 lanes), "wide" / "wide2" (GSP_TEST_PV_DRAIN_WIDE=1 / 2: those rows as class 1, 512 lanes,
-# or class 2, 1024 lanes), "hbm" (GSP_TEST_PV_DRAIN_LDS=300: every long row in the HBM kernel)
+# the drain kernels' row classes (pv_drain_class): "lds" as sized (class 0: <= 3,072 tuples,
+# 192 lanes), "wide1" / "wide" / "wide2" (GSP_TEST_PV_DRAIN_WIDE=1 / 2 / 3: those rows as class
+# 1, 256 lanes, class 2, 512 lanes, or class 3, 1024 lanes), "hbm" (GSP_TEST_PV_DRAIN_LDS=300:
+# every long row in the HBM kernel)
 def _set_class(monkeypatch, cls):
-    if cls in ("wide", "wide2"):
-        monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", "1" if cls == "wide" else "2")
+    wide = {"wide1": "1", "wide": "2", "wide2": "3"}
+    if cls in wide:
+        monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", wide[cls])
     elif cls == "hbm":
         monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
 
 
-@pytest.mark.parametrize("cls", ["lds", "wide", "wide2"])
+@pytest.mark.parametrize("cls", ["lds", "wide1", "wide", "wide2"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d" % c[:3])
 def test_drain_all_matches_oracle(case, cls, monkeypatch):
     _set_class(monkeypatch, cls)
@@ -102,7 +105,7 @@ def test_drain_all_matches_oracle(case, cls, monkeypatch):
     assert longest > 7
 
 
-@pytest.mark.parametrize("cls", ["lds", "wide", "wide2", "hbm"])
+@pytest.mark.parametrize("cls", ["lds", "wide1", "wide", "wide2", "hbm"])
 @pytest.mark.parametrize("evict_order", [0, 1])
 def test_drain_all_events_and_rows_run(monkeypatch, evict_order, cls):
     """Every join / remove / evict record of the long rows, every row run exactly once (the
