@@ -438,11 +438,11 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->drain = p->inbox == 0;
     if (s->drain) {
         // the HBM drain kernel (class 4 rows) runs one 1024-lane workgroup per CU, each with two
-        // HBM tuple buffers: a power of two >= n + 3 kPvMaxView (a list of distinct ids plus one
-        // message's runs always fits, so any row finishes in chunks), at most 2^19 tuples (a
-        // list past it stops the job, GSP_ERR_CAPACITY)
+        // HBM tuple buffers: a power of two >= n + 3 kPvMaxView, so a list of distinct ids plus
+        // one message's runs always fits and any row finishes in chunks (n <= 2^21 - 768; ids
+        // are 21 bits): 2 x 16 MB per CU at n = 1M, in drain mode only
         s->scratch_cap = 8192;
-        while (s->scratch_cap < int64_t(p->n) + 3 * gsp::kPvMaxView && s->scratch_cap < (int64_t(1) << 19))
+        while (s->scratch_cap < int64_t(p->n) + 3 * gsp::kPvMaxView && s->scratch_cap < (int64_t(1) << 21))
             s->scratch_cap <<= 1;
         if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
             s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(gsp::kDrainLdsMax, std::atoi(dl)));

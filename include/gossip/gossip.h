@@ -484,9 +484,8 @@ int gsp_events_write_log(uint64_t *ev, int64_t n, const char *path);
  * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (1..7,
  * ascending sender; the rest are counted as overflow) -- or, with inbox = 0, every message it
  * was sent, as the reference's checkMessages drains its queue (MP1Node.cpp:200-212; the plain
- * protocol and join schedules without an introducer list: tfail, swim and intro_list 0; a
- * receiver whose merged list would pass the drain kernel's 2^19-tuple HBM buffers stops the
- * job with GSP_ERR_CAPACITY, which needs n near 2^19); after the TREMOVE scan a view larger than `view` keeps the entries with the smallest
+ * protocol and join schedules without an introducer list: tfail, swim and intro_list 0; the
+ * drain kernels hold any receiver's list for n <= 2^21 - 768); after the TREMOVE scan a view larger than `view` keeps the entries with the smallest
  * (age, -hb, id).  DESIGN.md "Partial view".
  * ---------------------------------------------------------------------------------- */
 typedef struct gsp_pview gsp_pview;
