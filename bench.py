@@ -9,17 +9,21 @@ peers (the reference's nodeLoop, /root/reference/MP1Node.cpp:176-362, at scale).
 
 Headline (`value`, `roofline`): BASELINE config 3 -- 65,536 nodes, full view (65,536 x
 65,536 packed u16 table), fanout 3, 1% random crash at t = 10, no drops; ticks 1..W warm up,
-W+1..W+K timed.  N > 1: the same workload (strong scaling), column-sharded over N GPUs, one
+W+1..W+K timed, with the device event stream on (every join / remove recorded: the
+reference's Log lines, Log.cpp:116-130; the events-off run is reported beside it in
+`events_off`).  N > 1: the same workload (strong scaling), column-sharded over N GPUs, one
 process per GPU; the engine exchanges per-row counts and peer choices over its own RCCL
 communicator, torch.distributed only carries the RCCL id, the barrier and the timing
 reductions (DESIGN.md "Multi-GPU").
 Second line item (`pview`): BASELINE config 5 -- 1,048,576 nodes, bounded partial view
-V = 256, fanout 3, inbox 7, 10% drops, 5% contiguous crash at t = 10; N > 1: row-sharded
-over N GPUs with the per-tick sender-view exchange over RCCL send/recv (strong scaling);
-reports its own node-rounds/s, tick-kernel roofline and xGMI bytes per tick, the share of
-delivered messages the inbox bound discards (inbox_overflow_frac) and the share of removals
-that hit live nodes (removes_of_live_frac, from the event run).  `pview_drain`: the same
-workload with every message merged (inbox 0, as the reference drains its queue).
+V = 256, fanout 3, every delivered message merged (inbox 0, as the reference's checkMessages
+drains its queue, MP1Node.cpp:200-212), 10% drops, 5% contiguous crash at t = 10; N > 1:
+row-sharded over N GPUs with the per-tick sender-view exchange over RCCL send/recv (strong
+scaling); reports its own node-rounds/s, tick-kernel roofline, the drain row classes' rows,
+messages and kernel time (`drain_classes`), xGMI bytes per tick and the share of removals
+that hit live nodes (removes_of_live_frac, from the event run).  `pview_inbox7`: the same
+workload with the bounded inbox (at most 7 messages merged per receiver and tick; the share
+of delivered messages it discards is inbox_overflow_frac).
 Prints ONE JSON line (rank 0) with the roofline of the fused tick kernel and the CPU
 baseline (the oracle restatement, timed on a bounded sample of the same workload).
 """
@@ -165,15 +169,17 @@ def cpu_baseline(budget_s=12.0):
 
 
 PV_NODES = 1 << 20
-PV_KW = dict(view=256, fanout=3, inbox=7, drop_pct=10, fail_mode=2, fail_tick=10, fail_ppm=50000,
+PV_KW = dict(view=256, fanout=3, inbox=0, drop_pct=10, fail_mode=2, fail_tick=10, fail_ppm=50000,
              seed=SEED)
+DRAIN_CLASSES = ["hash0 (256 lanes, 3,584 slots)", "hash1 (256, 4,672)", "hash2 (256, 6,080)",
+                 "hash3 (256, 8,960)", "hash4 (512, 18,944)", "hub (1,024 lanes, HBM buffers)"]
 
 
-def pview_cpu_baseline(budget_s=10.0):
+def pview_cpu_baseline(budget_s=10.0, inbox=0):
     """oracle/pview_oracle.c (1 thread) on n = 5000 with config 5's V, fanout, inbox, drops
     and failure rule: per-node work does not depend on n in a bounded view."""
     from tests.oracle_binding import PviewOracle
-    o = PviewOracle(5000, **PV_KW)
+    o = PviewOracle(5000, **dict(PV_KW, inbox=inbox))
     t0 = time.perf_counter()
     ticks = rounds = 0
     while time.perf_counter() - t0 < budget_s and ticks < 40:
@@ -182,7 +188,8 @@ def pview_cpu_baseline(budget_s=10.0):
     el = time.perf_counter() - t0
     o.close()
     return {"value": rounds / el, "unit": "node-rounds/s", "cores": 1, "kind": "port",
-            "sample": "oracle/pview_oracle.c, n=5000, V=256, %d ticks in %.1f s" % (ticks, el)}
+            "sample": "oracle/pview_oracle.c, n=5000, V=256, inbox %d, %d ticks in %.1f s" %
+                      (inbox, ticks, el)}
 
 
 def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1, events=0,
@@ -209,6 +216,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     if events:
         eng.drain_events()
     p0 = eng.perf()
+    d0 = eng.drain_stats() if kw["inbox"] == 0 else None
     if dist is not None:
         dist.barrier()
     _sync()
@@ -220,6 +228,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     el = time.perf_counter() - t0
     eng.sync()
     p1 = eng.perf()
+    d1 = eng.drain_stats() if kw["inbox"] == 0 else None
     rounds = delivered = merges = csr = overflow = 0
     for t in range(warmup + 1, warmup + steps + 1):
         d = eng.digest(t)
@@ -234,6 +243,19 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     xch_ms = (p1["csr_ms"] - p0["csr_ms"]) / launches
     bytes_per_tick = ((2.0 * rounds + delivered) * V * 8.0 + csr * 4.0) / steps
     xgmi = (p1["xgmi_bytes"] - p0["xgmi_bytes"]) / steps
+    classes = None
+    if d0 is not None:
+        # per drain class and tick: rows, messages merged, kernel ms and its algorithmic GB/s
+        # (own view read + write and one sender view per message)
+        classes = []
+        for c, name in enumerate(DRAIN_CLASSES):
+            rows_c = (d1["rows"][c] - d0["rows"][c]) / steps
+            msgs_c = (d1["messages"][c] - d0["messages"][c]) / steps
+            ms_c = (d1["ms"][c] - d0["ms"][c]) / steps
+            b = (2.0 * rows_c + msgs_c) * V * 8.0
+            classes.append({"class": name, "rows_per_tick": rows_c, "messages_per_tick": msgs_c,
+                            "kernel_ms_per_tick": ms_c,
+                            "achieved_gbs": b / (ms_c * 1e-3) / 1e9 if ms_c > 0 else None})
     ev = None
     if events:
         from gossip_protocol_amd import _lib
@@ -257,10 +279,8 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
     achieved = bytes_per_tick / (kern_ms * 1e-3) / 1e9
     peak = PEAK_HBM_GBS * world
     window = [warmup + 1, warmup + steps]
-    # the committed PMC passes are of the inbox-7 protocol: nothing for the drain-all run
-    headline = kw["inbox"] == PV_KW["inbox"]
-    traffic, traffic_note = _pview_traffic(nodes, world, window) if headline else (None, None)
     k_in = kw["inbox"]
+    traffic, traffic_note = _pview_traffic(nodes, world, window, k_in)
     out = {
         "metric": "gossip node-rounds/sec (partial view)", "value": rounds / el,
         "unit": "node-rounds/s", "ms_per_step": el * 1e3 / steps, "scaling": "strong",
@@ -278,16 +298,18 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": ("pview_tick_split_kernel (256- and 128-lane rows, per tick)" if k_in else
-                                "pview_tick_split_kernel + pview_drain_{lds,hbm}_kernel (rows sent > 7 "
+                                "pview_tick_split_kernel + pview_drain_{hash,hbm}_kernel (rows sent > 7 "
                                 "messages), per tick"),
-                     "valu": _pview_valu(nodes, world, kern_ms, window) if headline else None,
+                     "valu": _pview_valu(nodes, world, kern_ms, window, k_in),
                      "window_ticks": window,
                      "kernel_ms_per_tick": kern_ms, "algorithmic_bytes_per_tick": bytes_per_tick},
     }
     if traffic_note:
         out["roofline"]["traffic_note"] = traffic_note
+    if classes is not None:
+        out["drain_classes"] = classes
     if world == 1 and cpu_baseline_on:
-        out["cpu_baseline"] = pview_cpu_baseline()
+        out["cpu_baseline"] = pview_cpu_baseline(inbox=k_in)
     return out
 
 
@@ -314,30 +336,38 @@ def _window_note(name, have, window):
             (name, have[0], have[1], window[0], window[1])) if have else None
 
 
-def _pview_traffic(nodes, world, window):
+def _pv_pmc_name(kind, inbox):
+    """profiles/pmc_<kind>_pview.json: the drain-all run (inbox 0, the headline);
+    pmc_<kind>_pview_inbox7.json: the bounded-inbox run."""
+    return "pmc_%s_pview%s.json" % (kind, "" if inbox == 0 else "_inbox%d" % inbox)
+
+
+def _pview_traffic(nodes, world, window, inbox):
     """HBM bytes per tick from the committed PMC passes (FETCH_SIZE x2 + WRITE_SIZE,
-    scripts/pmc_traffic.py --pview) for the one-GPU config-5 run over the same tick window,
-    else (None, note)."""
+    scripts/pmc_traffic.py --pview) for the one-GPU config-5 run of this inbox over the same
+    tick window, else (None, note)."""
     if nodes != PV_NODES or world != 1:
         return None, None
-    d, w = _pmc("pmc_traffic_pview.json", window)
+    name = _pv_pmc_name("traffic", inbox)
+    d, w = _pmc(name, window)
     if d is None:
-        return None, _window_note("pmc_traffic_pview.json", w, window)
+        return None, _window_note(name, w, window)
     return d.get("bytes_per_launch"), None
 
 
-def _pview_valu(nodes, world, kern_ms, window):
+def _pview_valu(nodes, world, kern_ms, window, inbox):
     """The tick kernel's actual limiter: VALU issue.  SQ_INSTS_VALU per tick from the committed
-    PMC pass over the same tick window (profiles/pmc_sq_pview.json) over the live mean kernel
+    PMC pass over the same tick window (profiles/pmc_sq_pview*.json) over the live mean kernel
     time: wave64 VALU instructions issued per SIMD cycle (1,024 SIMDs at 2.4 GHz), and that rate
     against the SIMD's issue ceiling -- one wave64 VALU instruction per 2 cycles with two or more
     waves resident (MI355X_MICROARCH.md, "Wave scheduling" and the v_fma_f32 row of the
     constants table; 4 cycles is one wave alone); config 5, one GPU."""
     if nodes != PV_NODES or world != 1:
         return None
-    d, w = _pmc("pmc_sq_pview.json", window)
+    name = _pv_pmc_name("sq", inbox)
+    d, w = _pmc(name, window)
     if d is None:
-        note = _window_note("pmc_sq_pview.json", w, window)
+        note = _window_note(name, w, window)
         return {"note": note} if note else None
     try:
         insts = d["counters"]["SQ_INSTS_VALU"]["per_launch"]
@@ -557,11 +587,13 @@ def main(argv=None):
     ap.add_argument("--item-budget", type=int, default=420,
                     help="seconds for the secondary line items before the line is printed as is")
     ap.add_argument("--no-events", action="store_true",
-                    help="skip the event-stream run (detection latency, recording cost)")
+                    help="the headline without the event stream, and no event-stream runs")
     ap.add_argument("--no-rows", action="store_true",
                     help="skip the full-view row-layout line items (N > 1)")
-    ap.add_argument("--no-drain", action="store_true",
-                    help="skip the drain-all config-5 line item (inbox 0)")
+    ap.add_argument("--no-events-off", action="store_true",
+                    help="skip the events-off run of the headline workload")
+    ap.add_argument("--no-inbox7", action="store_true",
+                    help="skip the bounded-inbox config-5 line item (inbox 7)")
     args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -574,10 +606,13 @@ def main(argv=None):
         if not dist.is_initialized():
             torch.cuda.set_device(local)
             dist.init_process_group("nccl")
-    full = run_full(args.nodes, args.steps, args.warmup, world, local, dist)
+    # the headline records every join / remove on the device (the reference's Log lines)
+    full = run_full(args.nodes, args.steps, args.warmup, world, local, dist,
+                    events=not args.no_events)
     out = None
     if rank == 0:
         out = summarize_full(full, args.nodes, args.steps, world, args.warmup)
+        out["event_stream"] = "on" if not args.no_events else "off"
         out.update({"n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                     "higher_is_better": True, "vs_baseline": None})
         if world == 1 and not args.no_cpu_baseline:
@@ -614,19 +649,19 @@ def main(argv=None):
             else:
                 out.setdefault(key, {})[sub] = res
 
-    # the same headline workload with the event stream on: kernel-time cost of recording
-    # every join / remove on the device, and the detection latency read from the records
-    def _events_item():
-        r = run_full(args.nodes, args.steps, args.warmup, world, local, dist, events=True)
+    # the detection latency read from the headline's records, and the same workload with the
+    # event stream off beside it: the kernel-time cost of recording
+    if not args.no_events and out is not None:
+        out["events"] = full["events"]
+    def _events_off_item():
+        r = run_full(args.nodes, args.steps, args.warmup, world, local, dist, events=False)
         if r is None or out is None:
             return None
-        ev = r["events"]
-        ev.update({"kernel_ms": r["kern_ms"], "kernel_ms_events_off": full["kern_ms"],
-                   "kernel_overhead_frac": r["kern_ms"] / full["kern_ms"] - 1.0,
-                   "value_events_on": r["rounds"] / r["el"]})
-        return ev
-    if not args.no_events:
-        item("events", _events_item)
+        return {"value": r["rounds"] / r["el"], "ms_per_step": r["el"] * 1e3 / args.steps,
+                "kernel_ms_per_tick": r["kern_ms"], "kernel_ms_events_on": full["kern_ms"],
+                "events_on_overhead_frac": full["kern_ms"] / r["kern_ms"] - 1.0}
+    if not args.no_events and not args.no_events_off:
+        item("events_off", _events_off_item)
     if not args.no_pview:
         item("pview", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world,
                                         local, dist, not args.no_cpu_baseline))
@@ -648,13 +683,13 @@ def main(argv=None):
         return r
     if not args.no_pview and not args.no_events:
         item("pview", lambda: _pv_events("pview"), "events")
-    if not args.no_pview and not args.no_drain:
-        # config 5 with every delivered message merged (inbox 0), as the reference drains its
-        # queue (MP1Node.cpp:200-212): the cost of the protocol without the inbox bound
-        item("pview_drain", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup,
-                                              world, local, dist, False, inbox=0))
+    if not args.no_pview and not args.no_inbox7:
+        # config 5 with the bounded inbox (at most 7 messages merged per receiver and tick):
+        # the protocol of rounds 1-5's headline, beside the drain-all one
+        item("pview_inbox7", lambda: run_pview(args.pview_nodes, min(args.steps, 30), args.warmup,
+                                               world, local, dist, False, inbox=7))
         if not args.no_events:
-            item("pview_drain", lambda: _pv_events("pview_drain", inbox=0), "events")
+            item("pview_inbox7", lambda: _pv_events("pview_inbox7", inbox=7), "events")
     if not args.no_262k:
         # BASELINE config 4: 262,144 nodes full view, 8,192-column tiles: on one GPU 32 tiles
         # (the table pair is 2 x 128 GiB of the 288 GB HBM), at N > 1 32 / N tiles per rank

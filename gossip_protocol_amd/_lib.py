@@ -206,6 +206,8 @@ SIGNATURES = {
     "gsp_pview_own_hb": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int32)]),
     "gsp_pview_messages": (ctypes.c_int, [ctypes.c_void_p, P(c_int32), c_int64, P(c_int64)]),
     "gsp_pview_perf_get": (ctypes.c_int, [ctypes.c_void_p, P(GspScalePerf)]),
+    "gsp_pview_drain_stats": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int64), P(c_int64),
+                                             P(ctypes.c_double)]),
     "gsp_pview_rows_run": (ctypes.c_int, [ctypes.c_void_p, c_int32, P(c_int64)]),
     "gsp_scale_drain_events": (ctypes.c_int, [ctypes.c_void_p, P(c_uint64), c_int64, P(c_int64),
                                               P(c_int64)]),

@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -88,9 +89,15 @@ struct gsp_pview {
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
     int64_t scratch_cap = 0;     // HBM drain kernel: tuples per buffer (two per workgroup)
-    int32_t drain_lds = gsp::kDrainLdsMax;   // drain kernels: LDS tuples (GSP_TEST_PV_DRAIN_LDS lowers it)
+    int32_t drain_lds = gsp::kDrainLdsMax;   // hash classes: ids a row may meet (GSP_TEST_PV_DRAIN_LDS lowers it)
     int32_t drain_wide = 0;      // tests: GSP_TEST_PV_DRAIN_WIDE=w runs the rows of classes < w in class w
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
+    int32_t *h_dhead = nullptr;  // drain all: pinned copy of a shard's long_list head (class sizes)
+    // drain all: per class, rows and messages run and kernel ms (gsp_pview_drain_stats)
+    using DrainEvents = std::array<hipEvent_t, gsp::kDrainClasses + 1>;
+    std::vector<DrainEvents> dpending;
+    int64_t drain_rows[gsp::kDrainClasses] = {}, drain_msgs[gsp::kDrainClasses] = {};
+    double drain_ms[gsp::kDrainClasses] = {};
     std::vector<PvShard> local;
     std::vector<int32_t> h_fail, h_start;
     bool joins = false;          // a join schedule is set (some node starts after tick 0)
@@ -168,6 +175,7 @@ struct gsp_pview {
             a.cus = cus;
             a.drain_lds = drain_lds;
             a.drain_wide = drain_wide;
+            a.drain_rows = h_dhead;
         }
         return a;
     }
@@ -212,9 +220,10 @@ int pview_validate(const gsp_pview_params *p) {
                 p->view, gsp::kPvMaxView);
     GSP_REQUIRE(p->inbox >= 0 && p->inbox <= gsp::kPvMaxInbox, GSP_ERR_INVALID,
                 "inbox=%d outside [0, %d] (0: every message merged)", p->inbox, gsp::kPvMaxInbox);
-    GSP_REQUIRE(p->inbox > 0 || (p->tfail == 0 && p->swim == 0 && p->policy.intro_list == 0),
-                GSP_ERR_INVALID, "inbox=0 (drain all) runs the plain protocol (and join schedules "
-                "without an introducer list): tfail, swim and intro_list must be 0");
+    // drain all: the hub kernel's HBM buffers hold any receiver's list plus one message's runs
+    // (a power of two >= n + 3 kPvMaxView tuples, at most 2^21)
+    GSP_REQUIRE(p->inbox > 0 || p->n <= (1 << 21) - 3 * gsp::kPvMaxView, GSP_ERR_INVALID,
+                "inbox=0 (drain all) needs n <= %d", (1 << 21) - 3 * gsp::kPvMaxView);
     GSP_REQUIRE(p->fanout >= 1 && p->fanout <= 16, GSP_ERR_INVALID, "fanout=%d outside [1,16]",
                 p->fanout);
     GSP_REQUIRE(p->tremove >= 1 && p->tremove <= 31, GSP_ERR_INVALID, "tremove=%d outside [1,31]",
@@ -320,15 +329,21 @@ int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
 
 // The capacity flag as last mirrored to the host: a receiver sent more than max_segment
 // messages at tick t sets the flag to t, and the tick kernels of t and every later tick run no
-// row, so the job's state stays that of tick t - 1.  Every shard held by this engine reads one
-// flag (shard 0's), so an in-process group stops as a whole; ranks of a communicator
-// exchange their flags with the row-exchange counts and stop at the same tick.
+// row, so the job's state stays that of tick t - 1.  A drain-all hub row past its HBM buffers
+// (tick t | kDrainErrBit) is found while tick t's rows run: rows already done hold tick t, the
+// others are skipped, so the views after that error are undefined (the job stops all the same).
+// Every shard held by this engine reads one flag (shard 0's), so an in-process group stops as a
+// whole; ranks of a communicator exchange their flags with the row-exchange counts and stop at
+// the same tick.
 int pview_mirrored_err(gsp_pview *s) {
     for (size_t i = 0; i < s->local.size(); ++i) {
         const int32_t e = s->h_err[i];
         GSP_REQUIRE(!(e & gsp::kRowxErrBit), GSP_ERR_CAPACITY,
                     "row exchange at tick %d: a shard's rows or records passed the region capacity "
                     "or the size posted to RCCL; the job stopped there", e & ~gsp::kRowxErrBit);
+        GSP_REQUIRE(!(e & gsp::kDrainErrBit), GSP_ERR_CAPACITY,
+                    "drain all at tick %d: a hub row's list passed its HBM buffers; the job stopped "
+                    "there (the views of that tick are undefined)", e & ~gsp::kDrainErrBit);
         GSP_REQUIRE(e == 0, GSP_ERR_CAPACITY,
                     "a receiver was sent more than %d messages at tick %d; the job stopped there",
                     s->max_segment, e);
@@ -400,6 +415,16 @@ int pview_collect(gsp_pview *s) {
         s->free_events.push_back(t.c);
     }
     s->pending.clear();
+    for (auto &de : s->dpending) {
+        GSP_HIP(hipEventSynchronize(de[gsp::kDrainClasses]));
+        for (int c = 0; c < gsp::kDrainClasses; ++c) {
+            float ms = 0.f;
+            GSP_HIP(hipEventElapsedTime(&ms, de[size_t(c)], de[size_t(c) + 1]));
+            s->drain_ms[c] += ms;
+        }
+        for (hipEvent_t e : de) s->free_events.push_back(e);
+    }
+    s->dpending.clear();
     if (s->rowmode)
         if (int rc = gsp::rowx_collect(s->rowx, &s->perf.xgmi_bytes)) return rc;
     for (size_t i = 0; i < s->local.size(); ++i)
@@ -430,6 +455,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     if (s->split && s->sort_rows) {
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
         GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
+        if (p->inbox == 0) GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_dhead), gsp::kDrainHead * 4));
     }
     GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
@@ -446,7 +472,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
             s->scratch_cap <<= 1;
         if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
             s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(gsp::kDrainLdsMax, std::atoi(dl)));
-        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(3, std::atoi(dw)));
+        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(4, std::atoi(dw)));
     }
     s->pos_scatter = !s->rowmode && !s->joins;
     if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
@@ -527,6 +553,8 @@ int gsp_pview_destroy(gsp_pview *s) {
         s->free_events.push_back(t.b);
         s->free_events.push_back(t.c);
     }
+    for (auto &de : s->dpending)
+        for (hipEvent_t e : de) s->free_events.push_back(e);
     for (hipEvent_t e : s->free_events) (void)hipEventDestroy(e);
     for (PvShard &sh : s->local) {
         if (sh.prof.p) {   // GSP_PV_PROFILE diagnostics: cycles per phase of sampled rows, by k
@@ -556,6 +584,7 @@ int gsp_pview_destroy(gsp_pview *s) {
     s->rowx.release();
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->h_kcount) (void)hipHostFree(s->h_kcount);
+    if (s->h_dhead) (void)hipHostFree(s->h_dhead);
     if (s->kcount_ev) (void)hipEventDestroy(s->kcount_ev);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
@@ -607,7 +636,21 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
         if (s->comm)
             GSP_NCCL(ncclAllReduce(s->local[0].err.p, s->local[0].err.p, 1, ncclInt32, ncclMax, s->comm, s->st));
         if (s->timing) GSP_HIP(hipEventRecord(tm.b, s->st));
-        for (PvShard &sh : s->local) GSP_HIP(gsp::launch_pview_tick(s->args(sh, t), s->st));
+        for (PvShard &sh : s->local) {
+            gsp::PviewTickArgs ta = s->args(sh, t);
+            gsp_pview::DrainEvents de{};
+            if (s->drain && s->timing) {
+                for (hipEvent_t &e : de) e = s->event();
+                ta.drain_ev = de.data();
+            }
+            GSP_HIP(gsp::launch_pview_tick(ta, s->st));
+            if (ta.drain_ev) s->dpending.push_back(de);
+            if (s->drain && s->h_dhead)          // the class sizes this launch read back
+                for (int c = 0; c < gsp::kDrainClasses; ++c) {
+                    s->drain_rows[c] += s->h_dhead[c];
+                    s->drain_msgs[c] += s->h_dhead[8 + c];
+                }
+        }
         if (s->timing) {
             GSP_HIP(hipEventRecord(tm.c, s->st));
             s->pending.push_back(tm);
@@ -716,6 +759,18 @@ int gsp_pview_rows_run(gsp_pview *s, int32_t t, int64_t *rows) {
         total += c;
     }
     *rows = total;
+    return GSP_OK;
+}
+
+int gsp_pview_drain_stats(gsp_pview *s, int32_t classes, int64_t *rows, int64_t *messages, double *ms) {
+    GSP_REQUIRE(s && classes >= 0, GSP_ERR_INVALID, "gsp_pview_drain_stats: bad argument");
+    if (int rc = gsp_pview_sync(s)) return rc;
+    for (int32_t c = 0; c < classes; ++c) {
+        const bool in = c < gsp::kDrainClasses;
+        if (rows) rows[c] = in ? s->drain_rows[c] : 0;
+        if (messages) messages[c] = in ? s->drain_msgs[c] : 0;
+        if (ms) ms[c] = in ? s->drain_ms[c] : 0.0;
+    }
     return GSP_OK;
 }
 

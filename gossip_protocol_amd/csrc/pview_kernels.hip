@@ -244,29 +244,6 @@ struct RowOut {
     bool written;                 // the view is already in HBM (pv_own_only)
 };
 
-// The bounded introducer list (block-uniform): bit q of m = rank q of node 0's gossiped members
-// is carried -- B sequential distinct Philox ranks (next_distinct_rank, philox.hpp) kept as a
-// 256-bit mask instead of a sorted array, so nothing is indexed dynamically (no scratch).
-__device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r, int32_t cnt,
-                                     int32_t B, uint64_t (&m)[4]) {
-    m[0] = m[1] = m[2] = m[3] = 0ull;
-    for (int32_t i = 0; i < B; ++i) {
-        int32_t rk = int32_t(draw_u31(kDomainJoin, seed, t_send, 0u, r, uint32_t(i)) % uint32_t(cnt - i));
-        bool done = false;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {                    // the rk-th rank not chosen yet
-            const int32_t zeros = 64 - __popcll(m[w]);
-            if (!done && rk < zeros) {
-                uint64_t z = ~m[w];
-                for (int32_t q = 0; q < rk; ++q) z &= z - 1;
-                m[w] |= z & (~z + 1);
-                done = true;
-            }
-            if (!done) rk -= zeros;
-        }
-    }
-}
-
 // Steps 2-5 for a row with k <= kBlocks - 1 merged messages (kBlocks = 1, 2, 3, 4, 6 or 8).
 // ent0: this lane's slot of the own view; ssrc/sslot: the receipt record (wave-uniform).
 // kExt: the protocol extensions compiled in, a bit mask -- kExtPol: TFAIL payload filter, JOINREP (jrep:
@@ -926,16 +903,7 @@ __device__ __forceinline__ void pv_row(const PviewTickArgs &a, Sh &sh, int32_t l
     // the swim paths survived its drop draw (paths sent at t - 1)
     uint32_t pcol = kNoId;
     bool pok = false;
-    if ((kExt & kExtPol) && a.swim > 0) {
-        const int32_t p = __builtin_amdgcn_readfirstlane(a.ping[lr]);
-        if (p >= 0) {
-            pcol = uint32_t(p);
-            for (int32_t i = 0; i < a.swim; ++i)
-                pok = pok || int32_t(draw_u31(kDomainPing, a.seed, uint32_t(a.tick - 1), uint32_t(r),
-                                              uint32_t(p), uint32_t(i)) % 100u) >= a.drop_prev;
-            pok = pok && a.tick <= a.fail_tick[p] && (!a.start_tick || a.tick >= a.start_tick[p]);
-        }
-    }
+    if constexpr ((kExt & kExtPol) != 0) pv_swim_probe(a, lr, uint32_t(r), pcol, pok);
     pm.mark(0);
     if constexpr ((kExt & ~kExtRot) == 0 && kQlo == 0) {   // (a row without messages evicts nothing)
         if (k == 0) {
@@ -1111,21 +1079,23 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
     }
     if (a.drain) {           // the long rows by drain class: one global atomic per class and
                              // workgroup (per wave, 16 K waves per tick on 4 counters, cost 0.17 ms)
-        __shared__ int32_t cls_cnt[kDrainClasses][4], cls_base[kDrainClasses];
+        __shared__ int32_t cls_cnt[kDrainClasses][4], cls_msg[kDrainClasses][4], cls_base[kDrainClasses];
         const int32_t wave = int32_t(threadIdx.x) >> 6;
         const int32_t c = lng ? pv_drain_class(k_all, a.view, a.drain_lds, a.drain_wide) : -1;
         unsigned long long mine = 0;
 #pragma unroll
         for (int q = 0; q < kDrainClasses; ++q) {
             const unsigned long long lm = __ballot(c == q);
-            if (lane == 0) cls_cnt[q][wave] = __popcll(lm);
+            const uint32_t msgs = wave_sum32(c == q ? uint32_t(k_all) : 0u);
+            if (lane == 0) { cls_cnt[q][wave] = __popcll(lm); cls_msg[q][wave] = int32_t(msgs); }
             mine = c == q ? lm : mine;
         }
         __syncthreads();
-        if (threadIdx.x < kDrainClasses) {
+        if (threadIdx.x < kDrainClasses) {       // rows of each class at [c], messages at [8 + c]
             const int32_t q = int32_t(threadIdx.x);
             const int32_t tot = cls_cnt[q][0] + cls_cnt[q][1] + cls_cnt[q][2] + cls_cnt[q][3];
             cls_base[q] = tot ? atomicAdd(&a.long_list[q], tot) : 0;
+            if (tot) atomicAdd(&a.long_list[8 + q], cls_msg[q][0] + cls_msg[q][1] + cls_msg[q][2] + cls_msg[q][3]);
         }
         __syncthreads();
         if (c >= 0) {
@@ -1393,6 +1363,8 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         PviewTickArgs b = a;
         int32_t c[8];
         if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            (a.drain && a.drain_rows &&
+             hipMemcpyAsync(a.drain_rows, a.long_list, kDrainHead * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
             hipEventRecord(a.kcount_event, st) != hipSuccess || hipEventSynchronize(a.kcount_event) != hipSuccess)
             return hipGetLastError();
         for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
@@ -1436,7 +1408,9 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         default: hipLaunchKernelGGL((pview_tick_kernel<kExtRot | kExtPol | kExtEv>), g, blk, 0, st, a); break;
     }
     if (a.drain) {
-        const hipError_t e = launch_pview_drain(a, st);
+        PviewTickArgs b = a;
+        b.drain_rows = nullptr;                  // not copied back in this form: persistent grids
+        const hipError_t e = launch_pview_drain(b, st);
         if (e != hipSuccess) return e;
     }
     launch_send_and_digest(a, st);

@@ -5,6 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "philox.hpp"
+#include "pview_kernels.hpp"
+
 namespace gsp {
 
 // Event digest term (oracle/pview_oracle.c gsp_pv_event_mix): S + g(x) per event, S a row seed
@@ -37,5 +40,49 @@ __device__ inline uint32_t pv_bin(uint32_t v, uint32_t t5, uint32_t th0) {
 }
 // the sender entry of a GOSSIP: hb + 1 and ts = t, or (1, t) when absent (MP1Node.cpp:237-243)
 __device__ inline uint32_t pv_event(uint32_t v, uint32_t t5) { return (((v >> 5) + 1u) << 5) | t5; }
+
+// The bounded introducer list (block-uniform): bit q of m = rank q of node 0's gossiped members
+// is carried -- B sequential distinct Philox ranks (next_distinct_rank, philox.hpp) kept as a
+// 256-bit mask instead of a sorted array, so nothing is indexed dynamically (no scratch).
+__device__ inline void pv_intro_mask(uint64_t seed, uint32_t t_send, uint32_t r, int32_t cnt,
+                                     int32_t B, uint64_t (&m)[4]) {
+    m[0] = m[1] = m[2] = m[3] = 0ull;
+    for (int32_t i = 0; i < B; ++i) {
+        int32_t rk = int32_t(draw_u31(kDomainJoin, seed, t_send, 0u, r, uint32_t(i)) % uint32_t(cnt - i));
+        bool done = false;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {                    // the rk-th rank not chosen yet
+            const int32_t zeros = 64 - __popcll(m[w]);
+            if (!done && rk < zeros) {
+                uint64_t z = ~m[w];
+                for (int32_t q = 0; q < rk; ++q) z &= z - 1;
+                m[w] |= z & (~z + 1);
+                done = true;
+            }
+            if (!done) rk -= zeros;
+        }
+    }
+}
+
+// SWIM: the probe row lr (node r) sent at t - 1 -- its target pcol (0xFFFFFFFF: none) and
+// whether it was answered (pok): the target is alive now and one of the swim paths survived
+// its drop draw (the drop percentage of the sends of t - 1).  Resolved after the merges, before
+// TREMOVE (oracle/pview_oracle.c pv_row_step).  Row-uniform.
+__device__ inline void pv_swim_probe(const PviewTickArgs &a, int32_t lr, uint32_t r, uint32_t &pcol, bool &pok) {
+    pcol = 0xFFFFFFFFu;
+    pok = false;
+    if (a.swim <= 0) return;
+    const int32_t p = __builtin_amdgcn_readfirstlane(a.ping[lr]);
+    if (p < 0) return;
+    pcol = uint32_t(p);
+    for (int32_t i = 0; i < a.swim; ++i)
+        pok = pok || int32_t(draw_u31(kDomainPing, a.seed, uint32_t(a.tick - 1), r, uint32_t(p), uint32_t(i)) %
+                             100u) >= a.drop_prev;
+    pok = pok && a.tick <= a.fail_tick[p] && (!a.start_tick || a.tick >= a.start_tick[p]);
+}
+// a TFAIL payload holds the sender's members gossipable at t - 1 ((t - 1) - ts < tfail)
+__device__ inline bool pv_gossiped(uint64_t v, uint32_t tf, uint32_t t5m1) {
+    return v != ~0ull && (tf == 0 || ((t5m1 - uint32_t(v)) & 31u) < tf);
+}
 
 }  // namespace gsp

@@ -118,6 +118,19 @@ class PviewEngine:
         check(lib().gsp_pview_rows_run(self._h, t, ctypes.byref(v)), "gsp_pview_rows_run")
         return v.value
 
+    def drain_stats(self, classes=6):
+        """Drain all (inbox 0): per row class since create, {"rows", "messages", "ms"} lists
+        (gsp_pview_drain_stats; classes 0-4 the LDS hash tables, 5 the hub kernel)."""
+        rows = np.zeros(classes, np.int64)
+        msgs = np.zeros(classes, np.int64)
+        ms = np.zeros(classes, np.float64)
+        P = ctypes.POINTER
+        check(lib().gsp_pview_drain_stats(self._h, classes, rows.ctypes.data_as(P(ctypes.c_int64)),
+                                          msgs.ctypes.data_as(P(ctypes.c_int64)),
+                                          ms.ctypes.data_as(P(ctypes.c_double))),
+              "gsp_pview_drain_stats")
+        return {"rows": rows.tolist(), "messages": msgs.tolist(), "ms": ms.tolist()}
+
     def perf(self):
         p = _lib.GspScalePerf()
         check(lib().gsp_pview_perf_get(self._h, ctypes.byref(p)), "gsp_pview_perf_get")

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GSP_ABI_VERSION 6
+#define GSP_ABI_VERSION 7
 
 typedef enum {
     GSP_OK = 0,
@@ -483,9 +483,9 @@ int gsp_events_write_log(uint64_t *ev, int64_t n, const char *path);
  * PARTIAL-VIEW engine (BASELINE config 5): every node keeps at most `view` member entries
  * (id, hb, ts) sorted by id; a receiver merges at most `inbox` messages per tick (1..7,
  * ascending sender; the rest are counted as overflow) -- or, with inbox = 0, every message it
- * was sent, as the reference's checkMessages drains its queue (MP1Node.cpp:200-212; the plain
- * protocol and join schedules without an introducer list: tfail, swim and intro_list 0; the
- * drain kernels hold any receiver's list for n <= 2^21 - 768); after the TREMOVE scan a view larger than `view` keeps the entries with the smallest
+ * was sent, as the reference's checkMessages drains its queue (MP1Node.cpp:200-212; every
+ * protocol option, for n <= 2^21 - 768: the hub kernel's buffers hold any receiver's list);
+ * after the TREMOVE scan a view larger than `view` keeps the entries with the smallest
  * (age, -hb, id).  DESIGN.md "Partial view".
  * ---------------------------------------------------------------------------------- */
 typedef struct gsp_pview gsp_pview;
@@ -538,6 +538,11 @@ int gsp_pview_row(gsp_pview *s, int32_t r, uint64_t *buf, int32_t cap, int32_t *
 int gsp_pview_own_hb(gsp_pview *s, int32_t r, int32_t *hb);
 int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);
+/* Drain all (inbox 0): per drain row class since create -- rows run, messages they merged and
+ * kernel ms (HIP events around each class's launch; 0 with timing off) -- for `classes`
+ * entries (class c < 5: the LDS hash tables, 5: the hub kernel; entries past them 0).  The
+ * counts are read back with the split kernels' bucket sizes (the default launch form). */
+int gsp_pview_drain_stats(gsp_pview *s, int32_t classes, int64_t *rows, int64_t *messages, double *ms);
 /* As gsp_scale_drain_events (join / remove / evict records). */
 int gsp_pview_drain_events(gsp_pview *s, uint64_t *buf, int64_t cap, int64_t *n, int64_t *lost);
 /* Test diagnostics: the rows the tick kernels of tick t ran, summed over the shards held here

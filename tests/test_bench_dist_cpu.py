@@ -45,6 +45,11 @@ class FakeEngine:
         return {"tick": t, "node_rounds": rows, "merges": 3 * rows, "delivered": 2 * rows,
                 "overflow": 0}
 
+    def drain_stats(self):
+        """Drain all: per class, 10 rows of 12 messages a tick in 0.5 ms (hub: none)."""
+        return {"rows": [10 * self.t] * 5 + [0], "messages": [120 * self.t] * 5 + [0],
+                "ms": [0.5 * self.t] * 5 + [0.0]}
+
     def drain_events(self):
         """Removal records split over the ranks (kind 2 = remove, 1 = join): node 5 is removed
         at ticks 12, 13 (rank 0) and 11 (rank 1), node 7 at 30 (rank 0) and 31 (rank 1)."""
@@ -135,10 +140,20 @@ def test_bench_two_ranks_gloo():
     assert ev["crashed_nodes"] == 2 and ev["removes_of_live_nodes"] == 0
     assert ev["first_detection_latency_ticks"] == {"min": 11, "mean": 20.5, "max": 30}
     assert ev["full_detection_latency_ticks"] == {"min": 13, "mean": 22.0, "max": 31}
-    assert ev["kernel_overhead_frac"] == 0.0
+    assert d["event_stream"] == "on"                  # the headline records the events
+    assert d["events_off"]["events_on_overhead_frac"] == 0.0
+    dc = pv["drain_classes"]                          # drain all: per class and tick
+    assert len(dc) == 6 and dc[0]["rows_per_tick"] == 10 and dc[0]["kernel_ms_per_tick"] == 0.5
+    assert dc[5]["achieved_gbs"] is None and pv["config"]["inbox"] == 0
+    p7 = d["pview_inbox7"]
+    assert p7["config"]["parallelism"] == "rows2" and p7["config"]["inbox"] == 7
+    assert "drain_classes" not in p7
     pe = pv["events"]                                 # the partial view's removes-only run
     assert "error" not in pe, pe
     assert pe["kinds"] == 4 and pe["crashed_nodes_detected"] == 2 and pe["kernel_overhead_frac"] == 0.0
+
+
+INBOXES_WITH_PMC = [7]        # committed profiles/pmc_*_pview*.json (0: drain all, 7: inbox 7)
 
 
 def test_counter_fields_only_for_their_window():
@@ -146,14 +161,15 @@ def test_counter_fields_only_for_their_window():
     that window prints them, any other window prints null with the window they belong to and
     no VALU fraction."""
     import bench
-    t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 25])
-    assert t is not None and note is None
-    t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 45])
-    assert t is None and "ticks 6-25" in note and "ticks 6-45" in note
-    v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 25])
-    assert v["frac_of_2cycle_issue"] > 0 and v["window_ticks"] == [6, 25]
-    v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 35])
-    assert set(v) == {"note"}
+    for inbox in INBOXES_WITH_PMC:
+        t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 25], inbox)
+        assert t is not None and note is None
+        t, note = bench._pview_traffic(bench.PV_NODES, 1, [6, 45], inbox)
+        assert t is None and "ticks 6-25" in note and "ticks 6-45" in note
+        v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 25], inbox)
+        assert v["frac_of_2cycle_issue"] > 0 and v["window_ticks"] == [6, 25]
+        v = bench._pview_valu(bench.PV_NODES, 1, 5.0, [6, 35], inbox)
+        assert set(v) == {"note"}
     r = {"bytes_per_tick": 4.2e10, "kern_ms": 6.5, "rounds": 1, "el": 1.0, "merges": 1,
          "xgmi_tick": 0.0, "layout": "columns", "tiles": 8, "csr_ms": 0.1}
     out = bench.summarize_full(r, bench.N_NODES, 20, 1, 5)

@@ -124,7 +124,7 @@ def test_struct_layouts_match_the_header():
                       ("gsp_pview_params", _lib.GspPviewParams),
                       ("gsp_pview_digest", _lib.GspPviewDigest)]:
         assert L.gsp_struct_size(name.encode()) == ctypes.sizeof(cls), name
-    assert L.gsp_abi_version() == 6
+    assert L.gsp_abi_version() == 7
 
 
 def test_scale_params_from_reference_conf():

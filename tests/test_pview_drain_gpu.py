@@ -2,13 +2,15 @@
 
 The reference drains every queued message (checkMessages, MP1Node.cpp:200-212); with inbox = 0
 so does the partial view: rows sent at most 7 messages run in the tick kernels, rows sent more
-run in pview_drain_kernel (gossip_protocol_amd/csrc/pview_drain.hip), which merges them all in
+run in gossip_protocol_amd/csrc/pview_drain.hip -- the hash classes (an LDS hash table per row,
+one message per step) or the hub kernel (sort and fold in HBM buffers) -- which merge them all in
 ascending sender order.  Every tick's digest (no overflow), the message lists and the views must
 equal the oracle's, which folds every message of every row the same way.  The cases make most
 rows long (fan-out 8 and 16 against small views), make hubs past 1,000 senders (a join burst
-of 2,000 nodes knowing only the introducer), and force the drain kernel's HBM paths (a row's
-update tuples or segment past its LDS capacity, GSP_TEST_PV_DRAIN_LDS lowers it; the hubs also
-take their messages in several chunks, the list carried between them).
+of 2,000 nodes knowing only the introducer), force every row class in turn (GSP_TEST_PV_DRAIN_WIDE
+moves the rows of the smaller hash classes up, GSP_TEST_PV_DRAIN_LDS sends every long row to the
+hub kernel, whose hubs also take their messages in several chunks, the list carried between
+them), and run the protocol extensions (TFAIL, SWIM, the JOINREP's introducer list) drained.
 """
 import numpy as np
 import pytest
@@ -82,19 +84,21 @@ CASES = [
 ]
 
 
-# the drain kernels' row classes (pv_drain_class): "lds" as sized (class 0: <= 3,072 tuples,
-# 192 lanes), "wide1" / "wide" / "wide2" (GSP_TEST_PV_DRAIN_WIDE=1 / 2 / 3: those rows as class
-# 1, 256 lanes, class 2, 512 lanes, or class 3, 1024 lanes), "hbm" (GSP_TEST_PV_DRAIN_LDS=300:
-# every long row in the HBM kernel)
+# the drain kernels' row classes (pv_drain_class): "h0" as sized (class 0: 3,328-slot tables),
+# "h1" .. "h4" (GSP_TEST_PV_DRAIN_WIDE=1..4: the rows of the smaller classes run in class w;
+# class 4 is the 512-lane, 19,712-slot table), "hub" (GSP_TEST_PV_DRAIN_LDS=300: every long row
+# in the hub kernel)
+CLASSES = ["h0", "h1", "h2", "h3", "h4", "hub"]
+
+
 def _set_class(monkeypatch, cls):
-    wide = {"wide1": "1", "wide": "2", "wide2": "3"}
-    if cls in wide:
-        monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", wide[cls])
-    elif cls == "hbm":
+    if cls.startswith("h") and cls != "hub" and cls != "h0":
+        monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", cls[1:])
+    elif cls == "hub":
         monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
 
 
-@pytest.mark.parametrize("cls", ["lds", "wide1", "wide", "wide2"])
+@pytest.mark.parametrize("cls", CLASSES[:5])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d" % c[:3])
 def test_drain_all_matches_oracle(case, cls, monkeypatch):
     _set_class(monkeypatch, cls)
@@ -105,7 +109,7 @@ def test_drain_all_matches_oracle(case, cls, monkeypatch):
     assert longest > 7
 
 
-@pytest.mark.parametrize("cls", ["lds", "wide1", "wide", "wide2", "hbm"])
+@pytest.mark.parametrize("cls", CLASSES)
 @pytest.mark.parametrize("evict_order", [0, 1])
 def test_drain_all_events_and_rows_run(monkeypatch, evict_order, cls):
     """Every join / remove / evict record of the long rows, every row run exactly once (the
@@ -115,6 +119,36 @@ def test_drain_all_events_and_rows_run(monkeypatch, evict_order, cls):
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=6, fail_ppm=30000,
               seed=17, tremove=10, evict_order=evict_order)
     _run(2500, 20, kw, events=True, rows_run=True, every=5)
+
+
+RANDOM, BLOCK, SINGLE, HALF = 1, 2, 3, 4
+EXT_CASES = [
+    # (n, view, fanout, drop, policy, shards, tfail, swim, ticks): the protocol extensions
+    # drained (MP1Node.h:22's TFAIL, SWIM probing, the JOINREP's introducer list)
+    (2000, 32, 8, 10, None, 1, 5, 0, 22),
+    (2000, 32, 8, 10, None, 1, 0, 2, 22),
+    (2000, 48, 6, 20, dict(drop_window=(3, 20), step_rate=0.02, intro_list=4,
+                           fail_events=[(10, SINGLE, 0), (14, BLOCK, 50000)]), 1, 5, 2, 24),
+    (3000, 32, 8, 10, dict(step_rate=0.006, intro_list=16, fail_events=[(9, HALF, 0)]), 1, 0, 0, 20),
+    (2000, 48, 6, 20, dict(drop_window=(3, 20), step_rate=0.02, intro_list=4), 3, 5, 2, 20),
+]
+
+
+@pytest.mark.parametrize("cls", ["h0", "h4", "hub"])
+@pytest.mark.parametrize("case", EXT_CASES, ids=lambda c: "n%d_v%d_f%d_%s_g%d_tf%d_sw%d" % (
+    c[0], c[1], c[2], "pol" if c[4] else "plain", c[5], c[6], c[7]))
+def test_drain_all_protocol_extensions(case, cls, monkeypatch):
+    """TFAIL (a payload holds what the sender gossiped at t - 1), SWIM (the probe of t - 1
+    answered or not before TREMOVE) and the JOINREP's bounded introducer list, every message
+    merged: GPU = oracle in the hash classes and the hub kernel, with events."""
+    _set_class(monkeypatch, cls)
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    n, V, f, drop, pol, shards, tfail, swim, ticks = case
+    kw = dict(view=V, fanout=f, inbox=0, drop_pct=drop, fail_mode=RANDOM, fail_tick=6,
+              fail_ppm=30000, seed=41, tfail=tfail, swim=swim)
+    longest = _run(n, ticks, kw, policy=pol, events=True, rows_run=pol is None, group=shards,
+                   every=4)
+    assert longest > 7
 
 
 @pytest.mark.parametrize("form", ["0:1", "1:1", "0:0"])
@@ -130,9 +164,9 @@ def test_drain_all_kernel_forms(monkeypatch, form):
 
 
 def test_drain_all_hbm_paths(monkeypatch):
-    """GSP_TEST_PV_DRAIN_LDS=300: every long row's update tuples (more than 300) are sorted and
-    folded in the HBM kernel's buffers instead of LDS."""
-    _set_class(monkeypatch, "hbm")
+    """GSP_TEST_PV_DRAIN_LDS=300: every long row (more than 300 ids) is sorted and folded in
+    the hub kernel's HBM buffers instead of an LDS hash table."""
+    _set_class(monkeypatch, "hub")
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=5, fail_ppm=20000, seed=31)
     _run(3000, 16, kw, every=4)
 
@@ -170,8 +204,7 @@ def test_drain_all_row_shards():
     _run(2400, 14, kw, group=3, every=7)
 
 
-def test_drain_all_rejects_protocol_extensions():
+def test_drain_all_rejects_n_past_the_hub_buffers():
     from gossip_protocol_amd._lib import GspError
-    for extra in (dict(tfail=5), dict(swim=2)):
-        with pytest.raises(GspError, match="drain all"):
-            PviewEngine(500, view=32, inbox=0, max_ticks=2, **extra)
+    with pytest.raises(GspError, match="drain all"):
+        PviewEngine((1 << 21) - 700, view=32, inbox=0, max_ticks=2)
