@@ -171,8 +171,8 @@ def cpu_baseline(budget_s=12.0):
 PV_NODES = 1 << 20
 PV_KW = dict(view=256, fanout=3, inbox=0, drop_pct=10, fail_mode=2, fail_tick=10, fail_ppm=50000,
              seed=SEED)
-DRAIN_CLASSES = ["hash0 (256 lanes, 3,584 slots)", "hash1 (256, 4,672)", "hash2 (256, 6,080)",
-                 "hash3 (256, 8,960)", "hash4 (512, 18,944)", "hub (1,024 lanes, HBM buffers)"]
+DRAIN_CLASSES = ["lds0 (192 lanes, <= 3,072 tuples)", "lds1 (256, 4,096)", "lds2 (512, 8,192)",
+                 "lds3 (1,024, 16,384)", "hub (1,024 lanes, HBM buffers)"]
 
 
 def pview_cpu_baseline(budget_s=10.0, inbox=0):
@@ -298,7 +298,7 @@ def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": peak, "unit": "GB/s",
                      "frac": achieved / peak, "traffic": traffic,
                      "kernel": ("pview_tick_split_kernel (256- and 128-lane rows, per tick)" if k_in else
-                                "pview_tick_split_kernel + pview_drain_{hash,hbm}_kernel (rows sent > 7 "
+                                "pview_tick_split_kernel + pview_drain_{lds,hbm}_kernel (rows sent > 7 "
                                 "messages), per tick"),
                      "valu": _pview_valu(nodes, world, kern_ms, window, k_in),
                      "window_ticks": window,

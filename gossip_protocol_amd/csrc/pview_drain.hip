@@ -11,31 +11,26 @@
 // distinct, and a sender is in no payload of its own), so within a message the updates are
 // independent, and across messages only each id's own updates need their order.
 //
-// HASH CLASSES (pview_drain_hash_kernel, round 6; every long row of up to kDrainStage messages
-// whose ids fit): the row's list is an LDS hash table of u64 slots id << 32 | own << 16 | val
-// (val = hb << 5 | ts5, 0 = absent; own: in the own view at the start, the join count's test),
-// linear probing from a multiplicative hash.  The own view is inserted, then the messages are
-// applied in ascending sender order, one message per step: lane p applies payload slot p
-// (pv_merge, MP1Node.cpp:247-251 present, :282-301 absent and fresh) and one lane the sender's
-// event (pv_event, :237-243) -- a 64-bit LDS compare-and-swap inserts an absent id, a found one
-// is updated in place -- and a barrier orders the steps.  The payloads are read 8 messages
-// ahead.  Then one pass counts joins, TREMOVE removals (and resolves the SWIM probe), a radix
-// select over the eviction key (age, -hb, id or rotated id) -- 8-bit digits, stopping at the
-// first digit whose boundary bin is taken whole -- finds the V-th survivor, and the kept
-// entries are written in id order (each one's rank among the kept).  This replaced round 5's
-// sort-and-fold of (k + 1) V tuples by a merge-path tree (4.4 ms of config 5's drain-all tick).
+// Every update of the row becomes a TUPLE, u64: id << 32 | m << 17 | flag << 16 | val (val =
+// hb << 5 | ts5): m = 0 the list (the own view at the start, flag = 1: the join count's test,
+// or the list a previous chunk left), m = 1..kc message m (its payload entries, flag 0, val 0
+// a no-op, and its sender, flag 1) -- built as runs of Vp = pow2(V) tuples, each sorted by id
+// (views are stored sorted), merged bottom-up by merge path, and each id's run folded in
+// message order: list tuple cur = val; payload cur = pv_merge (MP1Node.cpp:247-251 present,
+// :282-301 absent and fresh); sender cur = pv_event (:237-243).  Then TREMOVE and eviction to
+// V by two 256-bin histogram passes over the 16-bit prefix age << 11 | (2047 - hb) plus an
+// id-order (or rotated-id) cut of the boundary bin; the new view is written in id order.
 //
-// HUB CLASS (pview_drain_hbm_kernel: rows of more than kDrainStage messages or more ids than
-// the largest table): every update as a TUPLE, u64: id << 32 | m << 17 | flag << 16 | val
-// (m = 0 the list: the own view at the start, flag = 1, or the list a previous chunk left;
-// m = 1..kc message m of the chunk: its payload entries, flag 0, and its sender, flag 1),
-// built as runs of Vp = pow2(V) tuples each sorted by id, merged bottom-up (runs of Vp sorted
-// into 16 K-tuple blocks in LDS, the blocks merged in two HBM buffers per workgroup), each id's
-// run folded in message order, then TREMOVE and eviction to V by two 256-bin histogram passes
-// over the 16-bit prefix age << 11 | (2047 - hb) plus an id-order (or rotated-id) cut of the
-// boundary bin.  Messages are taken in chunks when they do not fit the buffers, the list
-// carried between chunks as the m = 0 run; a list past the buffers stops the job
-// (GSP_ERR_CAPACITY, err = tick | kDrainErrBit).
+// LDS CLASSES (pview_drain_lds_kernel; rows of at most kDrainStage messages and 16,384 tuples):
+// the row's tuples in one LDS buffer, merged and folded in place, 192 / 256 / 512 / 1024 lanes
+// per row by size (pv_drain_class), the counts into the per-row digest record.
+// HUB CLASS (pview_drain_hbm_kernel: the rest): runs sorted into 16 K-tuple blocks in LDS, the
+// blocks merged in two HBM buffers per workgroup; messages are taken in chunks when they do
+// not fit the buffers, the list carried between chunks as the m = 0 run; a list past the
+// buffers stops the job (GSP_ERR_CAPACITY, err = tick | kDrainErrBit).
+// Round 6 measured an LDS hash-table form of the LDS classes (the list as a hash table, one
+// message per step, a radix select for the eviction): parity-green but 7.1 ms against the
+// sort-and-fold's 4.4 ms on config 5's drain-all tick, so it was dropped.
 //
 // Both paths run the protocol extensions too: TFAIL (a payload holds the sender's members
 // gossipable at t - 1), SWIM (the probe of t - 1 resolved before TREMOVE) and the JOINREP's
@@ -63,18 +58,28 @@ constexpr uint64_t kStageJoinRep = 1ull << 39;  // a JOINREP: node 0's sender en
 constexpr uint64_t kStageRemote = 1ull << 38;   // the payload row is a received (remote) row
 constexpr uint64_t kStageRow = (1ull << 38) - 1;
 
-// LDS of one hub-kernel workgroup: CAP tuples (a block of runs sorted in place; the segment
-// sort keys), the eviction histogram, scan and digest words, the JOINREP payload mask.
+// LDS of one workgroup: CAP tuples (LDS classes: the row's tuple buffer; hub kernel: a block of
+// runs sorted in place, the segment sort keys), the senders of an LDS row, the eviction
+// histogram, scan and digest words, the JOINREP payload mask.
 template <int NT, int CAP>
 struct alignas(16) DrainShared {
     static constexpr int kW = NT / 64;
     uint64_t buf[CAP + CAP / 16];               // skewed (SkewBuf), one pad per 16
+    uint64_t stage[kDrainStage];                // LDS rows: the senders, staged (d_build)
     uint32_t hist[256];                         // eviction histogram
     uint32_t red[2][kW];                        // block scan words (two buffers, alternated)
     uint32_t sel[4];                            // selected bin, tuples still needed from it
     uint32_t tot[kW][8];                        // per-wave digest counts
     uint32_t jm[kPvMaxView / 32];               // JOINREP payload: slot p of node 0's view
 };
+
+// A workgroup barrier that orders LDS only: __syncthreads() would first wait for the wave's
+// global stores (a row's output, digest atomics) to complete, which nothing here needs.
+__device__ __forceinline__ void d_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 // An LDS tuple buffer indexed with one pad word per 16 tuples: a lane's contiguous run of 16
 // (the merge outputs, the fold's tuples) then starts 17 words after its neighbour's, so the
@@ -187,23 +192,35 @@ __device__ __forceinline__ uint64_t d_stage_word(const PviewTickArgs &a, int32_t
 
 // A JOINREP's payload with a bounded introducer list: node 0's members gossipable at t - 1
 // (TFAIL), those at the Philox ranks pv_intro_mask draws -- as bits over the slots of node 0's
-// view (jm[p / 32] bit p % 32).  Block-uniform; lane p looks at slot p (NT >= V).
+// view (jm[p / 32] bit p % 32).  Block-uniform; each lane looks at kPer contiguous slots.
 template <int NT>
 __device__ __forceinline__ void d_intro_mask(const PviewTickArgs &a, uint32_t r, uint32_t *jm, uint32_t *buf) {
-    static_assert(NT >= kPvMaxView, "a lane per view slot");
+    constexpr int kPer = (kPvMaxView + NT - 1) / NT;
     const int32_t tid = threadIdx.x;
-    const uint32_t t = uint32_t(a.tick);
-    const uint64_t e = tid < a.view ? a.intro[tid] : kPvEmpty;
-    const bool g = pv_gossiped(e, uint32_t(a.tfail), (t - 1u) & 31u);
+    const uint32_t t = uint32_t(a.tick), tf = uint32_t(a.tfail), t5m1 = (t - 1u) & 31u;
+    bool g[kPer];
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int32_t p = tid * kPer + q;
+        g[q] = pv_gossiped(p < a.view ? a.intro[p] : kPvEmpty, tf, t5m1);
+        c += g[q] ? 1u : 0u;
+    }
     if (tid < kPvMaxView / 32) jm[tid] = 0u;
     uint32_t cnt0 = 0;
-    const uint32_t rank = d_scan<NT>(g ? 1u : 0u, &cnt0, buf);   // (its barrier orders the zeroing)
+    uint32_t rank = d_scan<NT>(c, &cnt0, buf);                   // (its barrier orders the zeroing)
     const int32_t B = a.intro_list < int32_t(cnt0) ? a.intro_list : int32_t(cnt0);
     uint64_t cm[4];
     pv_intro_mask(a.seed, t - 1u, r, int32_t(cnt0), B, cm);
-    const uint32_t w = rank >> 6;
-    const uint64_t word = w == 0 ? cm[0] : w == 1 ? cm[1] : w == 2 ? cm[2] : cm[3];
-    if (g && ((word >> (rank & 63u)) & 1ull)) atomicOr(&jm[tid >> 5], 1u << (tid & 31));
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        if (!g[q]) continue;
+        const int32_t p = tid * kPer + q;
+        const uint32_t w = rank >> 6;
+        const uint64_t word = w == 0 ? cm[0] : w == 1 ? cm[1] : w == 2 ? cm[2] : cm[3];
+        if ((word >> (rank & 63u)) & 1ull) atomicOr(&jm[p >> 5], 1u << (p & 31));
+        rank++;
+    }
     __syncthreads();
 }
 
@@ -377,13 +394,13 @@ __device__ inline uint32_t d_prefix(uint32_t v, uint32_t t5) {   // age << 11 | 
     return (((t5 - v) & 31u) << 11) | (2047u - (v >> 5));
 }
 
-template <int NT, class Sh>
+template <int NT, bool kRecord = false, class Sh>
 __device__ __forceinline__ void d_row_digest(const PviewTickArgs &a, Sh &sh, int32_t lr, uint32_t r, int32_t k,
                                              uint32_t merged, uint32_t joins, uint32_t removes,
                                              uint32_t evicts, uint64_t hsum, uint32_t W);
 
 // Steps 5-6 over the list S[0, L) (x << 32 | own << 16 | val).  pcol / pok: the SWIM probe.
-template <bool kEv, int NT, class Sh, class P>
+template <bool kEv, int NT, bool kRecord = false, class Sh, class P>
 __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, int32_t L,
                                          int32_t lr, uint32_t r, int32_t k, uint32_t merged,
                                          uint32_t pcol, bool pok, DMark &pm) {
@@ -532,14 +549,16 @@ __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, in
     }
     for (int32_t i = int32_t(W) + tid; i < V; i += NT) __builtin_nontemporal_store(kPvEmpty, out + i);
     pm.mark(7);
-    d_row_digest<NT>(a, sh, lr, r, k, merged, joins, removes, evicts, hsum, W);
+    d_row_digest<NT, kRecord>(a, sh, lr, r, k, merged, joins, removes, evicts, hsum, W);
     pm.mark(8);
 }
 
-// The row's counts straight into the tick digest (its per-row record stays zero: a long row's
-// counts overflow the record's 8- and 16-bit fields) -- joins, removes, evictions, merges and
-// the hash (16 + 16 + 32 bits), one reduction -- and its length and own heartbeat.
-template <int NT, class Sh>
+// The row's counts: straight into the tick digest (a hub row's counts overflow the per-row
+// record's 8- and 16-bit fields; its record stays zero) or, kRecord (a hash-class row: k <= 64,
+// at most 19,712 ids), into the per-row record pview_digest_kernel sums (wave slot 0; no
+// contended global atomics) -- joins, removes, evictions, merges and the hash (16 + 16 + 32
+// bits), one reduction -- and its length and own heartbeat.
+template <int NT, bool kRecord, class Sh>
 __device__ __forceinline__ void d_row_digest(const PviewTickArgs &a, Sh &sh, int32_t lr, uint32_t r, int32_t k,
                                              uint32_t merged, uint32_t joins, uint32_t removes,
                                              uint32_t evicts, uint64_t hsum, uint32_t W) {
@@ -554,7 +573,7 @@ __device__ __forceinline__ void d_row_digest(const PviewTickArgs &a, Sh &sh, int
             if ((tid & 63) == 0) sh.tot[tid >> 6][q] = w;
         }
     }
-    __syncthreads();
+    d_sync_lds();                                                // (the row's stores need not wait)
     uint32_t sum[7] = {0, 0, 0, 0, 0, 0, 0};
     if (tid < 64) {                                              // wave 0: lane w reads wave w's
 #pragma unroll
@@ -562,24 +581,36 @@ __device__ __forceinline__ void d_row_digest(const PviewTickArgs &a, Sh &sh, int
     }
     const uint32_t jr = sum[0], rm = sum[1], evs = sum[2], mg = sum[3];
     const uint64_t h_lo = sum[4], h_mid = sum[5], h_hi = sum[6];
+    const uint64_t Sj = pv_seed(1, t, r), Sr = pv_seed(2, t, r), Se = pv_seed(3, t, r);
+    const uint64_t h = h_lo + (h_mid << 16) + (h_hi << 32) + uint64_t(jr) * Sj + uint64_t(rm) * Sr + uint64_t(evs) * Se;
+    if constexpr (kRecord) {
+        // rowdig[lr][0]: w0 = merges | delivered << 32 | round << 56, w1 = joins | removes << 16 |
+        // evicts << 32, w2 = the hash; w3 is the send kernel's; wave slots 1-3 zero
+        if (tid < 16 && tid != 3) {
+            const uint64_t w = tid == 0 ? uint64_t(mg + uint32_t(k)) | (uint64_t(k) << 32) | (1ull << 56)
+                               : tid == 1 ? uint64_t(jr) | (uint64_t(rm) << 16) | (uint64_t(evs) << 32)
+                               : tid == 2 ? h : 0ull;
+            a.rowdig[int64_t(lr) * 16 + tid] = w;
+        }
+    } else {
+        if (tid == 0) {
+            unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
+            atomicAdd(dig + kPvRounds, 1ull);
+            atomicAdd(dig + kPvMerges, (unsigned long long)(mg + uint32_t(k)));
+            atomicAdd(dig + kPvDelivered, (unsigned long long)k);
+            if (jr) atomicAdd(dig + kPvJoins, (unsigned long long)jr);
+            if (rm) atomicAdd(dig + kPvRemoves, (unsigned long long)rm);
+            if (evs) atomicAdd(dig + kPvEvicts, (unsigned long long)evs);
+            atomicAdd(dig + kPvHash, (unsigned long long)h);
+        }
+        if (tid < 16 && tid != 3) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;   // w3: the send kernel's
+    }
     if (tid == 0) {
-        const uint64_t Sj = pv_seed(1, t, r), Sr = pv_seed(2, t, r), Se = pv_seed(3, t, r);
-        unsigned long long *dig = a.dig + (blockIdx.x % kPvDigSlots) * kPvFields;
-        atomicAdd(dig + kPvRounds, 1ull);
-        atomicAdd(dig + kPvMerges, (unsigned long long)(mg + uint32_t(k)));
-        atomicAdd(dig + kPvDelivered, (unsigned long long)k);
-        if (jr) atomicAdd(dig + kPvJoins, (unsigned long long)jr);
-        if (rm) atomicAdd(dig + kPvRemoves, (unsigned long long)rm);
-        if (evs) atomicAdd(dig + kPvEvicts, (unsigned long long)evs);
-        const uint64_t h = h_lo + (h_mid << 16) + (h_hi << 32) + uint64_t(jr) * Sj + uint64_t(rm) * Sr +
-                           uint64_t(evs) * Se;
-        atomicAdd(dig + kPvHash, (unsigned long long)h);
         a.len_cur[lr] = int32_t(W);
         // alive at every tick since it started (pre-joined: ticks 1..t)
         const int32_t st = a.start_tick ? a.start_tick[r] : 0;
         a.own_hb[lr] = int32_t(t) - (st > 0 ? st - 1 : 0);
     }
-    if (tid < 16 && tid != 3) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;   // w3: the send kernel's
 }
 
 // The list's first form: the own view, this node itself and zero values left out, as list
@@ -607,7 +638,7 @@ __device__ __forceinline__ int32_t d_own(const PviewTickArgs &a, Sh &sh, P X, in
     return int32_t(tot);
 }
 
-// ---- LDS classes: the row's N <= CAP tuples in one LDS buffer, merged in place ----------
+// ---- the merge and the fold (LDS classes: the row's N <= CAP tuples in one LDS buffer) ------
 
 // Compare-exchange of two u64 registers (ascending)
 __device__ __forceinline__ void d_cx(uint64_t &x, uint64_t &y) {
@@ -725,6 +756,12 @@ __device__ __forceinline__ int32_t d_fold_block(Sh &sh, P S, int32_t sb, int32_t
         if (res[q]) S[int32_t(at++)] = res[q];
     __syncthreads();
     return int32_t(tot);
+}
+
+// The fold of an LDS row: one block.  Returns the list length.
+template <int NT, int F, class Sh, class P>
+__device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5, uint32_t tr) {
+    return d_fold_block<NT, F>(sh, S, 0, N, N, kNoId, 0, t5, tr);
 }
 
 // ---- hub kernel (class kDrainHub): two HBM tuple buffers per workgroup, messages in chunks --
@@ -845,407 +882,12 @@ __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a
     }
 }
 
-// ---- hash classes: the row's list in an LDS hash table, one message per step ---------------
+// ---- LDS classes: one row's tuples in one LDS buffer, merged and folded in place ----------
 
-template <int NT, int CAP>
-struct alignas(16) HashShared {
-    static constexpr int kW = NT / 64;
-    static constexpr int kCand = 640;           // kept entries (front), boundary-bin members (back)
-    uint64_t tab[CAP];                          // id << 32 | own << 16 | val; kNone: empty
-    uint64_t cand[kCand];                       // then the sort's exchange buffer
-    uint64_t stage[kDrainStage];                // the senders' staging words, ascending
-    union {
-        uint32_t bins[512];                     // survivors per (age, hb) bin, u16 pairs
-        uint32_t hist[256];                     // then the tie radix select's histogram
-    };
-    uint32_t red[2][kW];                        // block scan words (two buffers, alternated)
-    uint32_t sel[4];                            // selected bin, entries still needed from it
-    uint32_t cnt[2];                            // cand fill: kept, boundary-bin members
-    uint32_t tot[kW][8];                        // per-wave digest counts
-    uint32_t jm[kPvMaxView / 32];               // JOINREP payload: slot p of node 0's view
-};
-template <int NT, int CAP>
-constexpr int kHashPerCU = int(163840 / sizeof(HashShared<NT, CAP>));   // rows per CU by LDS
-
-// home bucket of id x: a multiplicative hash scaled onto [0, NB)
-template <int NB>
-__device__ __forceinline__ int32_t h_home(uint32_t x) {
-    return int32_t((uint64_t(x * 0x9E3779B1u) * uint64_t(NB)) >> 32);
-}
-
-enum : int { kHOwn = 0, kHPay = 1, kHSender = 2 };
-constexpr int kHBucket = 4;                     // slots per bucket (32 B: two 16-B LDS reads)
-
-// One update of id x: kHOwn inserts an own-view entry (val v, own bit), kHPay merges payload
-// value v (pv_merge), kHSender applies the sender's event (pv_event).  The table is CAP / 4
-// buckets of 4 slots probed bucket after bucket from x's home; a bucket's filled slots are a
-// prefix (an id takes the first empty slot it saw), so one read of a bucket finds x or proves
-// it absent when the bucket has room.  An absent id is inserted by the compare-and-swap of that
-// empty slot with the update applied to "absent" (an insert of value 0 -- a stale payload entry
-// of an absent id -- leaves an absent id behind, as the fold would); a lane that loses the slot
-// to another id re-reads the bucket.  A found id is updated in place by its one updater of this
-// step (the ids of one message are distinct).
-template <int CAP>
-__device__ __forceinline__ void h_update(uint64_t *tab, uint32_t x, int kind, uint32_t v, uint32_t t5, uint32_t tr) {
-    static_assert(CAP % kHBucket == 0, "whole buckets");
-    constexpr int NB = CAP / kHBucket;
-    const uint32_t init = kind == kHOwn ? ((1u << 16) | v) : kind == kHPay ? pv_merge(0u, v, t5, tr) : pv_event(0u, t5);
-    const unsigned long long ins = (static_cast<unsigned long long>(x) << 32) | init;
-    int32_t b = h_home<NB>(x);
-    for (;;) {
-        uint64_t *B = tab + kHBucket * b;
-        const ulonglong2 p0 = *reinterpret_cast<const ulonglong2 *>(B);
-        const ulonglong2 p1 = *reinterpret_cast<const ulonglong2 *>(B + 2);
-        const uint64_t sl[kHBucket] = {p0.x, p0.y, p1.x, p1.y};
-        int32_t f = -1, z = -1;
-#pragma unroll
-        for (int q = kHBucket - 1; q >= 0; --q) {
-            if (sl[q] == kNone) z = q;
-            else if (uint32_t(sl[q] >> 32) == x) f = q;
-        }
-        if (f >= 0) {
-            const uint64_t old = f == 0 ? sl[0] : f == 1 ? sl[1] : f == 2 ? sl[2] : sl[3];
-            const uint32_t cur = uint32_t(old) & 0xFFFFu;
-            const uint32_t nv = kind == kHPay ? pv_merge(cur, v, t5, tr) : pv_event(cur, t5);
-            if (nv != cur) B[f] = (old & ~0xFFFFull) | nv;
-            return;
-        }
-        if (z >= 0) {
-            const unsigned long long old =
-                atomicCAS(reinterpret_cast<unsigned long long *>(B + z), static_cast<unsigned long long>(kNone), ins);
-            if (old == kNone) return;
-            continue;                                            // another id took it: re-read
-        }
-        b = b + 1 < NB ? b + 1 : 0;                              // full: the next bucket
-    }
-}
-
-// The payload slot of this lane for messages [m0, m0 + B) (kPvEmpty past k or V); a JOINREP's
-// payload is node 0's view (masked by jm when applied) only with an introducer list
-template <int B, int NT, int CAP>
-__device__ __forceinline__ void h_load(const PviewTickArgs &a, const HashShared<NT, CAP> &sh, uint64_t (&e)[B],
-                                       int32_t m0, int32_t k, bool jpay) {
-    const int32_t tid = threadIdx.x, V = a.view;
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-        e[u] = kPvEmpty;
-        const int32_t m = m0 + u;
-        if (m > k) continue;                                     // block-uniform
-        const uint64_t w = sh.stage[m - 1];
-        const uint64_t *row = (w & kStageJoinRep) ? (jpay ? a.intro : nullptr)
-                              : ((w & kStageRemote) ? a.remote : a.prev) + int64_t(w & kStageRow) * V;
-        if (row && tid < V) e[u] = __builtin_nontemporal_load(row + tid);
-    }
-}
-
-// Messages [m0, m0 + B) applied in order, a barrier after each; returns the payload entries
-// merged (MP1Node.cpp:245's trips: what the sender gossiped)
-template <int B, int NT, int CAP>
-__device__ __forceinline__ uint32_t h_apply(HashShared<NT, CAP> &sh, const uint64_t (&e)[B], int32_t m0,
-                                            int32_t k, uint32_t r, uint32_t t5, uint32_t tr, uint32_t tf,
-                                            uint32_t t5m1) {
-    const int32_t tid = threadIdx.x;
-    uint32_t merged = 0;
-#pragma unroll
-    for (int u = 0; u < B; ++u) {
-        const int32_t m = m0 + u;
-        if (m > k) break;                                        // block-uniform
-        const uint64_t w = sh.stage[m - 1];
-        const bool jr = (w & kStageJoinRep) != 0;
-        const uint64_t x64 = e[u];
-        if (pv_gossiped(x64, tf, t5m1) && (!jr || ((sh.jm[tid >> 5] >> (tid & 31)) & 1u))) {
-            merged++;
-            const uint32_t x = uint32_t(x64 >> 32);
-            if (x != r) h_update<CAP>(sh.tab, x, kHPay, uint32_t(x64) & 0xFFFFu, t5, tr);   // never list yourself
-        }
-        if (tid == ((m - 1) & (NT - 1)))                         // the sender (a JOINREP's: node 0)
-            h_update<CAP>(sh.tab, jr ? 0u : uint32_t(w >> 40), kHSender, 0u, t5, tr);
-        __syncthreads();
-    }
-    return merged;
-}
-
-// A slot of an LDS list for every lane with `want`, one atomic per wave: the wave's count is
-// reserved by its first lane and each lane takes base + its rank among the wave's lanes.
-// Called by every lane of the wave.
-__device__ __forceinline__ uint32_t h_wave_slot(bool want, uint32_t *counter) {
-    const uint64_t m = __ballot(want);
-    const int32_t lane = int32_t(threadIdx.x & 63u);
-    uint32_t base = 0;
-    if (m) {
-        const int32_t first = __builtin_ffsll(static_cast<unsigned long long>(m)) - 1;
-        if (lane == first) base = atomicAdd(counter, uint32_t(__popcll(m)));
-        base = uint32_t(__builtin_amdgcn_readlane(int32_t(base), first));
-    }
-    return base + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
-}
-
-// the tie key of a boundary-bin member: (-hb, then the id or the rotated id)
-__device__ __forceinline__ uint32_t h_tie_key(uint32_t x, uint32_t v, bool rot, uint32_t mrot, uint32_t n) {
-    const uint32_t rid = rot ? (x >= mrot ? x - mrot : x + n - mrot) : x;
-    return ((2047u - (v >> 5)) << 21) | rid;
-}
-
-__device__ __forceinline__ uint64_t h_shfl_xor(uint64_t v, int m) {
-    const uint32_t lo = uint32_t(__shfl_xor(int(uint32_t(v)), m, 64));
-    const uint32_t hi = uint32_t(__shfl_xor(int(uint32_t(v >> 32)), m, 64));
-    return (uint64_t(hi) << 32) | lo;
-}
-
-// Bitonic sort, ascending, of the 256 values lane t < 256 holds (one each): strides below 64
-// inside the wave (lane shuffles), strides 64 and 128 through LDS (xbuf, 256 u64).  Every
-// thread of the workgroup takes part (lanes >= 256 only in the barriers).
-template <int NT>
-__device__ __forceinline__ uint64_t h_sort256(uint64_t v, uint64_t *xbuf) {
-    const int32_t t = threadIdx.x;
-#pragma unroll
-    for (int size = 2; size <= kPvMaxView; size <<= 1) {
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            uint64_t o;
-            if (stride >= 64) {
-                if (t < kPvMaxView) xbuf[t] = v;
-                __syncthreads();
-                o = t < kPvMaxView ? xbuf[t ^ stride] : v;
-                __syncthreads();
-            } else {
-                o = h_shfl_xor(v, stride);
-            }
-            const bool take_min = ((t & stride) == 0) == ((t & size) == 0);
-            const uint64_t mn = v < o ? v : o, mx = v < o ? o : v;
-            v = take_min ? mn : mx;
-        }
-    }
-    return v;
-}
-
-// Joins / TREMOVE (and the SWIM probe), eviction to V, the kept entries in id order, the
-// row's digest.  Eviction order (age, -hb, id or rotated id), in three steps:
-//   A. one pass over the table: the counts and event hashes, and a histogram of the survivors
-//      over the tick kernels' (age, hb) bins (pv_bin: age * 32 + min(h0 + t - age - hb, 31),
-//      ascending in (age, -hb); a bin below 31 holds one (age, hb)) -- the boundary bin b* holds
-//      the V-th survivor, every lower bin is kept;
-//   B. a second pass: the kept entries to the front of cand, b*'s members (tie key (2047 - hb,
-//      rotated id), slot) to its back;
-//   C. the need smallest tie keys of b* (a radix select over the member list, 8-bit digits,
-//      stopping at the first digit whose bin is taken whole; over the table when the list
-//      overflows) join the kept entries, the rest are evicted.
-// Evictions are counted and hashed as survivors minus kept.  The kept entries (at most 256,
-// distinct ids) are sorted by a bitonic network and written out.
+// One row of an LDS class, every message in one pass.
 template <bool kEv, int NT, int CAP>
-__device__ __forceinline__ void h_finish(const PviewTickArgs &a, HashShared<NT, CAP> &sh, int32_t lr, uint32_t r,
-                                         int32_t k, uint32_t merged, uint32_t pcol, bool pok, DMark &pm) {
-    using Sh = HashShared<NT, CAP>;
-    constexpr int F = (CAP + NT - 1) / NT;                       // table slots per lane
-    constexpr uint32_t kTieCap = uint32_t(Sh::kCand - kPvMaxView);
-    const int32_t tid = threadIdx.x, V = a.view;
-    const uint32_t t = uint32_t(a.tick), t5 = t & 31u, tr = uint32_t(a.tremove), th0 = t + uint32_t(a.h0);
-    const uint32_t Sj = uint32_t(pv_seed(1, t, r)), Sr = uint32_t(pv_seed(2, t, r)), Se = uint32_t(pv_seed(3, t, r));
-    const bool rot = a.evict_rot != 0;
-    const uint32_t n = uint32_t(a.n);
-    const uint32_t mrot = rot ? draw_u31(kDomainEvict, a.seed, t, r, 0u, 0u) % n : 0u;
-    const bool ev = kEv && a.ev.buf != nullptr;
-    const bool ev_ev = ev && (a.ev.kinds & GSP_EVENTS_EVICT);
-    uint32_t joins = 0, removes = 0, surv = 0;
-    uint64_t hsum = 0, hsurv = 0;                                // hsurv: evict hashes of the survivors
-    // A. joins (not in the own view at the start), the probe's answer, TREMOVE (MP1Node.cpp:
-    // 339-348), the survivors' (age, hb) histogram
-#pragma unroll 4
-    for (int q = 0; q < F; ++q) {
-        const int32_t i = q * NT + tid;
-        bool jn = false, rm = false;
-        uint32_t x = 0;
-        if (i < CAP) {
-            const uint64_t e = sh.tab[i];
-            uint32_t v = uint32_t(e) & 0xFFFFu;
-            if (e != kNone && v) {
-                x = uint32_t(e >> 32);
-                if (x == pcol) {                                 // SWIM: the probe's answer
-                    v = (v & 0xFFE0u) | (pok ? t5 : ((t5 - tr) & 31u));
-                    sh.tab[i] = (e & ~0xFFFFull) | v;
-                }
-                jn = !((uint32_t(e) >> 16) & 1u);
-                rm = ((t5 - v) & 31u) >= tr;
-                joins += jn ? 1u : 0u;
-                removes += rm ? 1u : 0u;
-                if (jn) hsum += pv_hash(Sj, x);
-                if (rm) {
-                    hsum += pv_hash(Sr, x);
-                } else {
-                    surv++;
-                    hsurv += pv_hash(Se, x);
-                    const uint32_t b = pv_bin(v, t5, th0);
-                    atomicAdd(&sh.bins[b >> 1], 1u << ((b & 1u) * 16u));
-                }
-            }
-        }
-        if (ev) {
-            const bool ej = jn && (a.ev.kinds & GSP_EVENTS_JOIN), er = rm && (a.ev.kinds & GSP_EVENTS_REMOVE);
-            uint64_t p = wave_reserve_events(ev_stripe_count(a.ev), (ej ? 1u : 0u) + (er ? 1u : 0u));
-            unsigned long long *eb = ev_stripe_buf(a.ev);
-            if (ej) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(1u, t, r, x); ++p; }
-            if (er) { if (int64_t(p) < a.ev.cap) eb[p] = event_record(2u, t, r, x); }
-        }
-    }
-    const uint32_t C = d_sum<NT>(surv, sh.red[0]);               // (its barrier: the bins are complete)
-    // the boundary bin b* and how many of it are kept (need); every lower bin is kept
-    uint32_t bstar = 1024u, need = 0;
-    if (int32_t(C) > V) {
-        if (tid < 64) {                                          // lane l sums bins [16 l, 16 l + 16)
-            const int32_t lane = tid;
-            const uint16_t *b16 = reinterpret_cast<const uint16_t *>(sh.bins);
-            const uint4 *bw = reinterpret_cast<const uint4 *>(sh.bins + 8 * lane);
-            uint32_t loc = 0;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint4 w = bw[q];
-                loc += (w.x & 0xFFFFu) + (w.x >> 16) + (w.y & 0xFFFFu) + (w.y >> 16) + (w.z & 0xFFFFu) +
-                       (w.z >> 16) + (w.w & 0xFFFFu) + (w.w >> 16);
-            }
-            const uint32_t incl = wave_incl_scan(loc);
-            const int32_t lb = __builtin_ffsll(__ballot(incl >= uint32_t(V))) - 1;
-            const uint32_t before = lane_of(incl - loc, lb);
-            const uint32_t c = lane < 16 ? uint32_t(b16[16 * lb + lane]) : 0u;
-            const uint32_t ci = wave_incl_scan(c);
-            const int32_t lh = __builtin_ffsll(__ballot(lane < 16 && before + ci >= uint32_t(V))) - 1;
-            if (lane == 0) {
-                sh.sel[0] = uint32_t(16 * lb + lh);
-                sh.sel[1] = uint32_t(V) - (before + lane_of(ci, lh) - lane_of(c, lh));
-            }
-        }
-        __syncthreads();
-        bstar = sh.sel[0];
-        need = sh.sel[1];
-    }
-    pm.mark(3);
-    // B. the kept entries to the front of cand, b*'s members to its back, the rest evicted
-#pragma unroll 4
-    for (int q = 0; q < F; ++q) {
-        const int32_t i = q * NT + tid;
-        bool evict = false, kp = false, tie = false;
-        uint32_t x = 0, tk = 0;
-        uint64_t ent = 0;
-        if (i < CAP) {
-            const uint64_t e = sh.tab[i];
-            const uint32_t v = uint32_t(e) & 0xFFFFu;
-            x = uint32_t(e >> 32);
-            if (e != kNone && v && ((t5 - v) & 31u) < tr) {
-                const uint32_t b = pv_bin(v, t5, th0);
-                kp = b < bstar;
-                tie = b == bstar;
-                evict = b > bstar;
-                if (tie) tk = h_tie_key(x, v, rot, mrot, n);
-                ent = (uint64_t(x) << 32) | uint64_t(v);
-            }
-        }
-        {                                                        // one counter atomic per wave
-            const uint32_t pk = h_wave_slot(kp, &sh.cnt[0]), pt = h_wave_slot(tie, &sh.cnt[1]);
-            if (kp) sh.cand[pk] = ent;
-            if (tie && pt < kTieCap) sh.cand[Sh::kCand - 1 - int32_t(pt)] = (uint64_t(tk) << 32) | uint32_t(i);
-        }
-        if (ev_ev) {
-            const uint64_t pe = wave_reserve_events(ev_stripe_count(a.ev), evict ? 1u : 0u);
-            if (evict && int64_t(pe) < a.ev.cap) ev_stripe_buf(a.ev)[pe] = event_record(3u, t, r, x);
-        }
-    }
-    __syncthreads();
-    const uint32_t nt = sh.cnt[1];
-    pm.mark(4);
-    // C. b*'s members: the need smallest tie keys are kept (key < Tt)
-    if (int32_t(C) > V) {
-        const bool listed = nt <= kTieCap;
-        auto visit = [&](auto &&f) {                             // f(tie key) per member
-            if (listed) {
-                for (int32_t j = tid; j < int32_t(nt); j += NT) f(uint32_t(sh.cand[Sh::kCand - 1 - j] >> 32));
-            } else {
-                for (int q = 0; q < F; ++q) {
-                    const int32_t i = q * NT + tid;
-                    if (i >= CAP) break;
-                    const uint64_t e = sh.tab[i];
-                    const uint32_t v = uint32_t(e) & 0xFFFFu;
-                    if (e != kNone && v && ((t5 - v) & 31u) < tr && pv_bin(v, t5, th0) == bstar)
-                        f(h_tie_key(uint32_t(e >> 32), v, rot, mrot, n));
-                }
-            }
-        };
-        uint64_t Tt = ~0ull;
-        if (nt > need) {
-            uint32_t nd = need;
-            uint64_t pre = 0;
-            for (int pass = 0; pass < 4; ++pass) {               // block-uniform
-                const int sft = 24 - 8 * pass;
-                for (int32_t i = tid; i < 256; i += NT) sh.hist[i] = 0u;
-                __syncthreads();
-                visit([&](uint32_t key) {
-                    if ((uint64_t(key) >> (sft + 8)) == pre) atomicAdd(&sh.hist[(key >> sft) & 255u], 1u);
-                });
-                __syncthreads();
-                d_select(sh, nd);
-                const uint32_t bin = sh.sel[0], nd2 = sh.sel[1], cnt = sh.hist[bin];
-                __syncthreads();                                 // sel / hist reused
-                pre = (pre << 8) | bin;
-                if (cnt == nd2) {
-                    Tt = (pre + 1) << sft;
-                    break;
-                }
-                nd = nd2;
-            }
-        }
-        // the kept members join the kept entries; the others are evicted
-        const int32_t trips = listed ? (int32_t(nt) + NT - 1) / NT : F;
-        for (int32_t q = 0; q < trips; ++q) {                    // block-uniform
-            bool evict = false;
-            uint32_t x = 0, v = 0, key = 0;
-            bool member = false;
-            if (listed) {
-                const int32_t j = q * NT + tid;
-                if (j < int32_t(nt)) {
-                    const uint64_t w = sh.cand[Sh::kCand - 1 - j];
-                    const uint64_t e = sh.tab[uint32_t(w)];
-                    x = uint32_t(e >> 32);
-                    v = uint32_t(e) & 0xFFFFu;
-                    key = uint32_t(w >> 32);
-                    member = true;
-                }
-            } else {
-                const int32_t i = q * NT + tid;
-                if (i < CAP) {
-                    const uint64_t e = sh.tab[i];
-                    x = uint32_t(e >> 32);
-                    v = uint32_t(e) & 0xFFFFu;
-                    member = e != kNone && v && ((t5 - v) & 31u) < tr && pv_bin(v, t5, th0) == bstar;
-                    key = member ? h_tie_key(x, v, rot, mrot, n) : 0u;
-                }
-            }
-            const bool kp = member && uint64_t(key) < Tt;
-            evict = member && !kp;
-            const uint32_t pk = h_wave_slot(kp, &sh.cnt[0]);
-            if (kp) sh.cand[pk] = (uint64_t(x) << 32) | uint64_t(v);
-            if (ev_ev) {
-                const uint64_t pe = wave_reserve_events(ev_stripe_count(a.ev), evict ? 1u : 0u);
-                if (evict && int64_t(pe) < a.ev.cap) ev_stripe_buf(a.ev)[pe] = event_record(3u, t, r, x);
-            }
-        }
-        __syncthreads();
-    }
-    const uint32_t W = sh.cnt[0];                                // min(C, V)
-    pm.mark(5);
-    // the kept entries in id order (distinct ids; the empty padding sorts last)
-    uint64_t my = tid < int32_t(W) ? sh.cand[tid] : kNone;
-    const uint64_t hkept = (tid < int32_t(W)) ? uint64_t(pv_hash(Se, uint32_t(my >> 32))) : 0ull;
-    __syncthreads();                                             // cand's reads before its reuse
-    my = h_sort256<NT>(my, sh.cand);
-    if (tid < V) __builtin_nontemporal_store(my, a.cur + int64_t(lr) * V + tid);
-    pm.mark(6);
-    const uint32_t evicts = tid == 0 ? C - W : 0u;
-    hsum += hsurv - hkept;                                       // the evicted ones' hashes (mod 2^64)
-    d_row_digest<NT>(a, sh, lr, r, k, merged, joins, removes, evicts, hsum, W);
-    pm.mark(7);
-}
-
-template <bool kEv, int NT, int CAP>
-__device__ __forceinline__ void h_row(const PviewTickArgs &a, HashShared<NT, CAP> &sh, int32_t lr, int32_t it) {
-    static_assert(NT >= kPvMaxView, "a lane per view slot");
+__device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, int32_t lr, int32_t it) {
+    constexpr int E = CAP / NT;
     const int32_t tid = threadIdx.x;
     const uint32_t r = uint32_t(a.row0 + lr);
     if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);       // tests: each row exactly once
@@ -1256,56 +898,46 @@ __device__ __forceinline__ void h_row(const PviewTickArgs &a, HashShared<NT, CAP
     }
     const int32_t V = a.view;
     const uint32_t t5 = uint32_t(a.tick) & 31u, tr = uint32_t(a.tremove);
-    const uint32_t tf = uint32_t(a.tfail), t5m1 = (uint32_t(a.tick) - 1u) & 31u;
     const int32_t o0 = a.csr_off[lr];
     const int32_t k = a.csr_off[lr + 1] - o0;                    // <= kDrainStage (the class)
     int32_t *src = a.csr_src + o0;
     int32_t *slot = a.csr_slot ? a.csr_slot + o0 : nullptr;
     DMark pm;
     pm.init(a.prof, it, k);
-    const uint64_t own = tid < V ? __builtin_nontemporal_load(a.prev + int64_t(lr) * V + tid) : kPvEmpty;
-    d_rank_segment<NT>(src, slot, k, a.row0, sh.tab);            // 1. ascending senders
-    for (int32_t i = tid; i < k; i += NT) sh.stage[i] = d_stage_word(a, src[i], slot, i);
-    for (int32_t i = tid; i < CAP; i += NT) sh.tab[i] = kNone;
-    for (int32_t i = tid; i < 512; i += NT) sh.bins[i] = 0u;
-    if (tid < 2) sh.cnt[tid] = 0u;
+    d_rank_segment<NT>(src, slot, k, a.row0, sh.buf);            // 1. ascending senders
     uint32_t pcol;
     bool pok;
     pv_swim_probe(a, lr, r, pcol, pok);
     const bool jpay = k > 0 && a.intro_list > 0 && src[0] == kJoinRepSrc;   // block-uniform
     if (jpay) d_intro_mask<NT>(a, r, sh.jm, sh.red[1]);
-    __syncthreads();
     pm.mark(0);
-    {                                                            // 2. the own view
-        const uint32_t x = uint32_t(own >> 32), v = uint32_t(own) & 0xFFFFu;
-        if (own != kPvEmpty && x != r && v != 0u) h_update<CAP>(sh.tab, x, kHOwn, v, t5, tr);
-    }
-    constexpr int B = 8;                                         // payloads read B messages ahead
-    uint64_t ea[B], eb[B];
-    h_load<B>(a, sh, ea, 1, k, jpay);
-    __syncthreads();
+    int32_t lgV = 0;
+    while ((1 << lgV) < V) ++lgV;
+    const int32_t Vp = 1 << lgV;
+    const SkewBuf X{sh.buf};
+    const int32_t L0 = d_own<NT>(a, sh, X, lr, r);               // <= V: padded to Vp
     pm.mark(1);
-    uint32_t merged = 0;                                         // 3. the messages, in order
-    for (int32_t m0 = 1; m0 <= k; m0 += 2 * B) {                 // block-uniform
-        h_load<B>(a, sh, eb, m0 + B, k, jpay);
-        merged += h_apply<B>(sh, ea, m0, k, r, t5, tr, tf, t5m1);
-        h_load<B>(a, sh, ea, m0 + 2 * B, k, jpay);
-        merged += h_apply<B>(sh, eb, m0 + B, k, r, t5, tr, tf, t5m1);
-    }
+    const uint32_t merged = d_build<NT>(a, X, sh.stage, L0, Vp, 0, k, Vp, lgV, src, slot, r, jpay ? sh.jm : nullptr);
     pm.mark(2);
-    h_finish<kEv, NT, CAP>(a, sh, lr, r, k, merged, pcol, pok, pm);
+    const int32_t N = Vp + (k << lgV) + ((k + Vp - 1) >> lgV << lgV);
+    d_merge_ip<NT, E>(X, N, Vp);
+    pm.mark(3);
+    const int32_t L = d_fold_ip<NT, E>(sh, X, N, t5, tr);
+    pm.mark(4);
+    // k <= 64 and L <= CAP: the counts fit the per-row record (no contended global atomics)
+    d_finish<kEv, NT, true>(a, sh, X, L, lr, r, k, merged, pcol, pok, pm);
 }
 
-// The rows of hash class kCls: workgroup b takes rows b, b + grid, ... (a persistent grid of
+// The rows of LDS class kCls: workgroup b takes rows b, b + grid, ... (a persistent grid of
 // rows-per-CU x CUs, or, with the host's copy of the class sizes, one row per workgroup)
-template <bool kEv, int NT, int CAP, int kCls, int kPerCU>
-__global__ void __launch_bounds__(NT, kPerCU) pview_drain_hash_kernel(PviewTickArgs a) {
-    __shared__ HashShared<NT, CAP> sh;
+template <bool kEv, int NT, int CAP, int kCls>
+__global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a) {
+    __shared__ DrainShared<NT, CAP> sh;
     const int32_t cnt = a.long_list[kCls];
     const int32_t *list = a.long_list + kDrainHead + int64_t(kCls) * a.rows;
     for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
-        h_row<kEv, NT, CAP>(a, sh, list[i], (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
-        __syncthreads();                                         // LDS free for the next row
+        d_row_lds<kEv, NT, CAP>(a, sh, list[i], (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
+        d_sync_lds();                                            // LDS free for the next row
     }
 }
 
@@ -1320,17 +952,16 @@ void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
     };
     auto mark = [&](int i) { if (a.drain_ev) (void)hipEventRecord(a.drain_ev[i], st); };
     mark(0);
-#define GSP_DRAIN_HASH(C, NT, CAP)                                                                    \
-    if (const unsigned g = grid(C, kHashPerCU<NT, CAP>))                                              \
-        hipLaunchKernelGGL((pview_drain_hash_kernel<kEv, NT, CAP, C, kHashPerCU<NT, CAP>>), dim3(g), dim3(NT), 0, \
-                           st, a);                                                                    \
+#define GSP_DRAIN_LDS(C, NT, CAP, PER_CU)                                                           \
+    if (const unsigned g = grid(C, PER_CU))                                                           \
+        hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, NT, CAP, C>), dim3(g), dim3(NT), 0, st, a);   \
     mark(C + 1);
-    GSP_DRAIN_HASH(0, 256, kDrainHashCap0)
-    GSP_DRAIN_HASH(1, 256, kDrainHashCap1)
-    GSP_DRAIN_HASH(2, 256, kDrainHashCap2)
-    GSP_DRAIN_HASH(3, 256, kDrainHashCap3)
-    GSP_DRAIN_HASH(4, 512, kDrainHashCap4)
-#undef GSP_DRAIN_HASH
+    // class c: rows of at most CAP update tuples (pv_drain_class), PER_CU rows per CU by LDS
+    GSP_DRAIN_LDS(0, 192, 3072, 5)
+    GSP_DRAIN_LDS(1, 256, 4096, 4)
+    GSP_DRAIN_LDS(2, 512, 8192, 2)
+    GSP_DRAIN_LDS(3, 1024, kDrainLdsMax, 1)
+#undef GSP_DRAIN_LDS
     if (grid(kDrainHub, 1)) hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(grid(kDrainHub, 1)), dim3(kHT), 0, st, a);
     mark(kDrainHub + 1);
 }

@@ -89,7 +89,7 @@ struct gsp_pview {
     bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
     int64_t scratch_cap = 0;     // HBM drain kernel: tuples per buffer (two per workgroup)
-    int32_t drain_lds = gsp::kDrainLdsMax;   // hash classes: ids a row may meet (GSP_TEST_PV_DRAIN_LDS lowers it)
+    int32_t drain_lds = gsp::kDrainLdsMax;   // drain kernels: LDS tuples (GSP_TEST_PV_DRAIN_LDS lowers it)
     int32_t drain_wide = 0;      // tests: GSP_TEST_PV_DRAIN_WIDE=w runs the rows of classes < w in class w
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     int32_t *h_dhead = nullptr;  // drain all: pinned copy of a shard's long_list head (class sizes)
@@ -170,7 +170,7 @@ struct gsp_pview {
             a.csr_off = sh.off.p;
             a.csr_src = sh.csr_src.p;
             a.csr_slot = rowmode ? sh.x.csr_slot.p : nullptr;
-            a.scratch = sh.scratch.p;
+            a.scratch = local[0].scratch.p;
             a.scratch_cap = scratch_cap;
             a.cus = cus;
             a.drain_lds = drain_lds;
@@ -294,7 +294,9 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
     if (s->drain) {
         GSP_HIP(sh.long_list.alloc(gsp::kDrainHead + size_t(gsp::kDrainClasses) * rows));
         GSP_HIP(hipMemsetAsync(sh.long_list.p, 0, gsp::kDrainHead * 4, st));
-        GSP_HIP(sh.scratch.alloc(size_t(s->cus) * 4 * size_t(s->scratch_cap)));   // 2 x u64 per CU
+        // 2 x u64 per CU, one set for every shard held here: their hub kernels run one after
+        // the other on the engine's stream
+        if (&sh == &s->local[0]) GSP_HIP(sh.scratch.alloc(size_t(s->cus) * 4 * size_t(s->scratch_cap)));
     }
     const size_t dig = size_t(s->p.max_ticks + 1) * gsp::kPvDigSlots * gsp::kPvFields;
     GSP_HIP(sh.dig.alloc(dig));
@@ -319,6 +321,11 @@ int shard_alloc(gsp_pview *s, PvShard &sh) {
 int exchange_and_csr(gsp_pview *s, int32_t t_sent) {
     gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, s->p.view, true, s->pair_cap, s->msg_cap,
                      s->comm, s->st, t_sent + 1, &s->rowx};
+    // a joiner's sends ramp up to F over its first ticks (its view grows): the joiners of the
+    // last three send ticks count as new senders
+    job.new_senders = s->joins ? s->plan.count(t_sent) + s->plan.count(t_sent - 1) + s->plan.count(t_sent - 2) : 0;
+    job.drop_now = gsp::drop_at(s->p.policy, s->p.drop_pct, t_sent);
+    job.drop_before = gsp::drop_at(s->p.policy, s->p.drop_pct, t_sent - 1);
     std::vector<gsp::RowxShard> v;
     for (PvShard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p, sh.table[t_sent & 1].p,
@@ -472,7 +479,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
             s->scratch_cap <<= 1;
         if (const char *dl = std::getenv("GSP_TEST_PV_DRAIN_LDS"))   // tests: reach the HBM paths
             s->drain_lds = std::max(gsp::kPvMaxView + 2, std::min(gsp::kDrainLdsMax, std::atoi(dl)));
-        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(4, std::atoi(dw)));
+        if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(3, std::atoi(dw)));
     }
     s->pos_scatter = !s->rowmode && !s->joins;
     if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;

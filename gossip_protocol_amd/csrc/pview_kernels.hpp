@@ -78,8 +78,8 @@ struct PviewTickArgs {
     uint32_t *scratch;           // [cus][2][scratch_cap] u64: HBM tuple buffers (hub rows)
     int64_t scratch_cap;         // tuples per buffer (>= 8192, a power of two)
     int32_t cus;                 // compute units: the hub kernel's persistent grid
-    int32_t drain_lds;           // largest hash-class need in use (tests lower it to reach the
-                                 // hub kernel, GSP_TEST_PV_DRAIN_LDS), <= kDrainLdsMax
+    int32_t drain_lds;           // LDS tuple capacity in use (tests lower it to reach the hub
+                                 // kernel, GSP_TEST_PV_DRAIN_LDS), <= kDrainLdsMax
     int32_t drain_wide;          // tests (GSP_TEST_PV_DRAIN_WIDE=w): the rows of classes < w run
                                  // in class w
     int32_t *drain_rows;         // pinned [kDrainHead]: long_list's head, copied back with the
@@ -89,32 +89,32 @@ struct PviewTickArgs {
                                  // after each (the per-class kernel time), or null
 };
 
-// Drain-all row classes (pview_drain.hip), by the ids a row can meet: the own view, k payloads
-// of V and k senders, need = (k + 1) V + k.  Classes 0-4 (k <= kDrainStage) fold every message
-// into an LDS hash table of kDrainHashCap[c] slots (8 B each), filled to at most 72 % (need <=
-// pv_drain_hash_lim(cap)): 256-lane rows, 4 / 3 / 2 / 2 per CU, and class 4 512-lane rows, 1 per CU
-// (k <= 9 / 12 / 16 / 24 / 52 at V = 256).  Class 5: the rest (the hubs), sorted and folded in
-// two HBM buffers per workgroup.  long_list: kDrainHead words -- the rows of each class at
-// [c], their messages at [8 + c] -- then the rows of each class.
-constexpr int kDrainClasses = 6;
-constexpr int kDrainHashClasses = 5;
-constexpr int kDrainHub = 5;
+// Drain-all row classes (pview_drain.hip), by the row's update tuples: own view + k payloads
+// (Vp = pow2(V) slots each) + the senders' runs.  In LDS (k <= kDrainStage): 0: <= 3,072
+// tuples, 192-lane rows, 5 per CU; 1: <= 4,096, 256-lane rows, 4 per CU; 2: <= 8,192, 512-lane
+// rows, 2 per CU; 3: <= 16,384, 1024-lane rows, 1 per CU (k <= 10 / 14 / 30 / 62 at V = 256).
+// Class 4 (kDrainHub): the rest, 1024-lane rows in two HBM buffers per workgroup (and every
+// row of a view below 8 slots).  long_list: kDrainHead words -- the rows of each class at [c],
+// their messages at [8 + c] -- then the rows of each class.
+constexpr int kDrainClasses = 5;
+constexpr int kDrainHub = 4;
 constexpr int kDrainHead = 16;
 constexpr int kDrainStage = 64;
+constexpr int kDrainLdsMax = 16384;
 // a hub row past its HBM buffers stops the job: err = tick | kDrainErrBit (kRowxErrBit: 1 << 24)
 constexpr int32_t kDrainErrBit = 1 << 25;
-constexpr int kDrainHashCap0 = 3584, kDrainHashCap1 = 4672, kDrainHashCap2 = 6080,
-              kDrainHashCap3 = 8960, kDrainHashCap4 = 18944;
-__host__ __device__ constexpr int32_t pv_drain_hash_lim(int32_t cap) { return int32_t(int64_t(cap) * 72 / 100); }
-constexpr int kDrainLdsMax = pv_drain_hash_lim(kDrainHashCap4);   // 13,639 ids
+__host__ __device__ inline int64_t pv_drain_need(int32_t k, int32_t view) {
+    int32_t vp = 1;
+    while (vp < view) vp <<= 1;
+    return int64_t(vp) * (1 + k) + (int64_t(k) + vp - 1) / vp * vp;
+}
 __host__ __device__ inline int32_t pv_drain_class(int32_t k, int32_t view, int32_t lds, int32_t wide) {
-    const int64_t need = int64_t(view) * (1 + k) + k;
-    if (k > kDrainStage || need > lds) return kDrainHub;
-    if (wide < 1 && need <= pv_drain_hash_lim(kDrainHashCap0)) return 0;
-    if (wide < 2 && need <= pv_drain_hash_lim(kDrainHashCap1)) return 1;
-    if (wide < 3 && need <= pv_drain_hash_lim(kDrainHashCap2)) return 2;
-    if (wide < 4 && need <= pv_drain_hash_lim(kDrainHashCap3)) return 3;
-    return need <= pv_drain_hash_lim(kDrainHashCap4) ? 4 : kDrainHub;
+    const int64_t need = pv_drain_need(k, view);
+    if (view < 8 || k > kDrainStage || need > lds) return kDrainHub;
+    if (wide < 1 && need <= 3072) return 0;
+    if (wide < 2 && need <= 4096) return 1;
+    if (wide < 3 && need <= 8192) return 2;
+    return need <= kDrainLdsMax ? 3 : kDrainHub;
 }
 constexpr int kPvProfPhases = 16;   // per (slot, k): phases 0..14, rows sampled
 

@@ -69,6 +69,7 @@ hipError_t RowxState::init(int32_t g, bool with_rccl) {
     max_pairs.assign(size_t(g) * g, -1);
     max_msgs.assign(size_t(g) * g, -1);
     if (const char *tt = std::getenv("GSP_TEST_ROWX_TIGHT")) tight = std::atoi(tt) != 0;
+    if (const char *tp = std::getenv("GSP_TEST_ROWX_POSTED")) posted = std::atoi(tp) != 0;
     return hipSuccess;
 }
 
@@ -161,16 +162,26 @@ int rowx_exchange(const RowxJob &job, std::vector<RowxShard> &local, double *byt
             if (int rc = rowx_see(st8, st8.seen, bytes)) return rc;
     const int32_t *d_bounds = nullptr;
     const size_t GG = size_t(G) * G;
-    if (job.comm || st8.tight) {
+    if (job.comm || st8.tight || st8.posted) {
         // sizes posted to RCCL, the same on every rank: derived from the all-gathered counts
-        // of exchanges 0 .. k - 1 (the capacity for the first exchange)
+        // of exchanges 0 .. k - 1 (the capacity for the first exchange), with margins for the
+        // drop draws' spread (1/16 + 256 pairs / 1024 records) and for the growth the host knows
+        // of: every new sender may add a pair and F records to every shard pair,
+        // and a drop percentage that falls scales what gets through by (100 - now) / (100 - before)
         int32_t *hb = st8.h_bounds + size_t(slot) * 2 * GG;
-        const int64_t mpa = st8.tight ? 0 : 256, mma = st8.tight ? 0 : 1024;
-        const int64_t div = st8.tight ? int64_t(1) << 40 : 16;
+        const bool tight = st8.tight;
+        const int64_t mpa = tight ? 0 : 256 + job.new_senders, mma = tight ? 0 : 1024 + job.new_senders * F;
+        const int64_t div = tight ? int64_t(1) << 40 : 16;
+        const bool rise = !tight && job.drop_now < job.drop_before;   // more of the sends get through
+        const int64_t num = 100 - job.drop_now, den = 100 - job.drop_before;
+        auto grow = [&](int64_t c, int64_t cap) {
+            if (rise) c = den > 0 ? (c * num + den - 1) / den : cap;
+            return std::min<int64_t>(cap, c);
+        };
         for (size_t i = 0; i < GG; ++i) {
             const int64_t mp = st8.max_pairs[i], mm = st8.max_msgs[i];
-            hb[i] = int32_t(mp < 0 ? job.pair_cap : std::min<int64_t>(job.pair_cap, mp + mp / div + mpa));
-            hb[GG + i] = int32_t(mm < 0 ? job.msg_cap : std::min<int64_t>(job.msg_cap, mm + mm / div + mma));
+            hb[i] = int32_t(mp < 0 ? job.pair_cap : std::min<int64_t>(job.pair_cap, grow(mp, job.pair_cap) + mp / div + mpa));
+            hb[GG + i] = int32_t(mm < 0 ? job.msg_cap : std::min<int64_t>(job.msg_cap, grow(mm, job.msg_cap) + mm / div + mma));
         }
         int32_t *db = x0.bounds.p + size_t(slot) * 2 * GG;
         GSP_HIP(hipMemcpyAsync(db, hb, 2 * GG * 4, hipMemcpyHostToDevice, st));

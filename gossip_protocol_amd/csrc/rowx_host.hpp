@@ -61,6 +61,8 @@ struct RowxState {
     bool rccl = false;
     bool tight = false;           // tests (GSP_TEST_ROWX_TIGHT=1): an in-process group posts and
                                   // checks sizes too, with no margin (the largest count seen)
+    bool posted = false;          // tests (GSP_TEST_ROWX_POSTED=1): an in-process group posts and
+                                  // checks the sizes a communicator would post (every margin)
 
     hipError_t init(int32_t shards, bool rccl);
     void release();
@@ -74,6 +76,12 @@ struct RowxJob {
     hipStream_t st;
     int32_t tick;                 // the tick whose tick kernels read this exchange
     RowxState *state;
+    // growth the host knows of between the last exchange whose counts it has read and this one
+    // (the posted sizes must cover it): senders whose first sends these are (a join schedule's
+    // nodes starting at the send tick), and the drop percentages of the sends of this exchange
+    // and of the one before
+    int64_t new_senders = 0;
+    int32_t drop_now = 0, drop_before = 0;
 };
 
 // Counts per shard in the all-gather: G pair counts, G record counts, its capacity flag.

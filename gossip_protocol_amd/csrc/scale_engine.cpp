@@ -398,6 +398,11 @@ int exchange_row_counts(gsp_scale *s, int32_t t) {
 int exchange_rows(gsp_scale *s, int32_t t_sent) {
     gsp::RowxJob job{s->p.n, s->shards, s->p.fanout, int32_t(s->stride / 4), false, s->pair_cap,
                      s->msg_cap, s->comm, s->st, t_sent + 1, &s->rowx};
+    // a joiner's sends ramp up to F over its first ticks (its view grows): the joiners of the
+    // last three send ticks count as new senders
+    job.new_senders = s->joins ? s->plan.count(t_sent) + s->plan.count(t_sent - 1) + s->plan.count(t_sent - 2) : 0;
+    job.drop_now = gsp::drop_at(s->p.policy, s->p.drop_pct, t_sent);
+    job.drop_before = gsp::drop_at(s->p.policy, s->p.drop_pct, t_sent - 1);
     std::vector<gsp::RowxShard> v;
     for (Shard &sh : s->local)
         v.push_back(gsp::RowxShard{sh.g, sh.row0, sh.rows, sh.out_dst.p,

@@ -118,9 +118,9 @@ class PviewEngine:
         check(lib().gsp_pview_rows_run(self._h, t, ctypes.byref(v)), "gsp_pview_rows_run")
         return v.value
 
-    def drain_stats(self, classes=6):
+    def drain_stats(self, classes=5):
         """Drain all (inbox 0): per row class since create, {"rows", "messages", "ms"} lists
-        (gsp_pview_drain_stats; classes 0-4 the LDS hash tables, 5 the hub kernel)."""
+        (gsp_pview_drain_stats; classes 0-3 the LDS classes, 4 the hub kernel)."""
         rows = np.zeros(classes, np.int64)
         msgs = np.zeros(classes, np.int64)
         ms = np.zeros(classes, np.float64)

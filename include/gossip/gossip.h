@@ -540,7 +540,7 @@ int gsp_pview_messages(gsp_pview *s, int32_t *dst, int64_t cap, int64_t *n);
 int gsp_pview_perf_get(gsp_pview *s, gsp_scale_perf *out);
 /* Drain all (inbox 0): per drain row class since create -- rows run, messages they merged and
  * kernel ms (HIP events around each class's launch; 0 with timing off) -- for `classes`
- * entries (class c < 5: the LDS hash tables, 5: the hub kernel; entries past them 0).  The
+ * entries (class c < 4: the LDS classes, 4: the hub kernel; entries past them 0).  The
  * counts are read back with the split kernels' bucket sizes (the default launch form). */
 int gsp_pview_drain_stats(gsp_pview *s, int32_t classes, int64_t *rows, int64_t *messages, double *ms);
 /* As gsp_scale_drain_events (join / remove / evict records). */

@@ -47,8 +47,8 @@ class FakeEngine:
 
     def drain_stats(self):
         """Drain all: per class, 10 rows of 12 messages a tick in 0.5 ms (hub: none)."""
-        return {"rows": [10 * self.t] * 5 + [0], "messages": [120 * self.t] * 5 + [0],
-                "ms": [0.5 * self.t] * 5 + [0.0]}
+        return {"rows": [10 * self.t] * 4 + [0], "messages": [120 * self.t] * 4 + [0],
+                "ms": [0.5 * self.t] * 4 + [0.0]}
 
     def drain_events(self):
         """Removal records split over the ranks (kind 2 = remove, 1 = join): node 5 is removed
@@ -143,8 +143,8 @@ def test_bench_two_ranks_gloo():
     assert d["event_stream"] == "on"                  # the headline records the events
     assert d["events_off"]["events_on_overhead_frac"] == 0.0
     dc = pv["drain_classes"]                          # drain all: per class and tick
-    assert len(dc) == 6 and dc[0]["rows_per_tick"] == 10 and dc[0]["kernel_ms_per_tick"] == 0.5
-    assert dc[5]["achieved_gbs"] is None and pv["config"]["inbox"] == 0
+    assert len(dc) == 5 and dc[0]["rows_per_tick"] == 10 and dc[0]["kernel_ms_per_tick"] == 0.5
+    assert dc[4]["achieved_gbs"] is None and pv["config"]["inbox"] == 0
     p7 = d["pview_inbox7"]
     assert p7["config"]["parallelism"] == "rows2" and p7["config"]["inbox"] == 7
     assert "drain_classes" not in p7

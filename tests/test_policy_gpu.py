@@ -196,3 +196,35 @@ def test_full_view_join_burst_past_1024_messages(layout, shards, tfail, swim, ev
             assert np.array_equal(hb_d[pres_d], hb_o[pres_d]), "hb row %d" % r
             assert np.array_equal(ts5_d[pres_d], ts_o[pres_d] & 31), "ts row %d" % r
     assert burst > 1024, "the case must send one receiver more than 1,024 messages (got %d)" % burst
+
+
+@pytest.mark.parametrize("engine", ["pview_inbox7", "pview_drain", "full_rows"])
+def test_row_exchange_posted_sizes_cover_join_bursts(monkeypatch, engine):
+    """The sizes a communicator posts to RCCL come from earlier ticks' counts plus margins
+    (rowx_host.cpp); the growth the host knows of -- a join burst's new senders, a drop window
+    that ends -- is added to them.  GSP_TEST_ROWX_POSTED=1 makes an in-process
+    group of 3 post and check exactly those sizes (a count past them stops the job with
+    GSP_ERR_CAPACITY), so a burst of thousands of joiners with the drop rate falling from 30 %
+    to 0 must run to the end and equal the oracle."""
+    monkeypatch.setenv("GSP_TEST_ROWX_POSTED", "1")
+    ticks = 12
+    if engine == "full_rows":
+        n, pol = 2100, dict(step_rate=0.002, intro_list=4, drop_window=(0, 5))
+        kw = dict(fanout=3, drop_pct=30, fail_mode=RANDOM, fail_tick=6, fail_ppm=20000, seed=53)
+        orc = ScaleOracle(n, policy=oracle_policy(**pol), **kw)
+        eng = ScaleEngine(n, max_ticks=ticks, group=3, layout="rows", policy=make_policy(**pol), **kw)
+    else:
+        n, pol = 6000, dict(step_rate=0.0005, intro_list=0, drop_window=(0, 5))
+        kw = dict(view=64, fanout=3, inbox=7 if engine == "pview_inbox7" else 0, drop_pct=30,
+                  fail_mode=RANDOM, fail_tick=6, fail_ppm=20000, seed=53)
+        orc = PviewOracle(n, policy=oracle_policy(**pol), **kw)
+        eng = PviewEngine(n, max_ticks=ticks, group=3, policy=make_policy(**pol), **kw)
+    with eng:
+        for t in range(1, ticks + 1):
+            want = orc.step()
+            eng.step(1)
+            assert eng.digest(t) == want, "tick %d" % t
+        src, dst = orc.messages()
+        m = eng.messages()
+        assert sorted((s, d) for s in range(n) for d in m[s] if d >= 0) == \
+            sorted(zip(src.tolist(), dst.tolist()))

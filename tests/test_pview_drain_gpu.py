@@ -2,13 +2,13 @@
 
 The reference drains every queued message (checkMessages, MP1Node.cpp:200-212); with inbox = 0
 so does the partial view: rows sent at most 7 messages run in the tick kernels, rows sent more
-run in gossip_protocol_amd/csrc/pview_drain.hip -- the hash classes (an LDS hash table per row,
-one message per step) or the hub kernel (sort and fold in HBM buffers) -- which merge them all in
-ascending sender order.  Every tick's digest (no overflow), the message lists and the views must
+run in gossip_protocol_amd/csrc/pview_drain.hip -- the LDS classes (the row's update tuples
+sorted and folded in one LDS buffer) or the hub kernel (the same in HBM buffers) -- which merge
+them all in ascending sender order.  Every tick's digest (no overflow), the message lists and the views must
 equal the oracle's, which folds every message of every row the same way.  The cases make most
 rows long (fan-out 8 and 16 against small views), make hubs past 1,000 senders (a join burst
 of 2,000 nodes knowing only the introducer), force every row class in turn (GSP_TEST_PV_DRAIN_WIDE
-moves the rows of the smaller hash classes up, GSP_TEST_PV_DRAIN_LDS sends every long row to the
+moves the rows of the smaller LDS classes up, GSP_TEST_PV_DRAIN_LDS sends every long row to the
 hub kernel, whose hubs also take their messages in several chunks, the list carried between
 them), and run the protocol extensions (TFAIL, SWIM, the JOINREP's introducer list) drained.
 """
@@ -84,21 +84,21 @@ CASES = [
 ]
 
 
-# the drain kernels' row classes (pv_drain_class): "h0" as sized (class 0: 3,328-slot tables),
-# "h1" .. "h4" (GSP_TEST_PV_DRAIN_WIDE=1..4: the rows of the smaller classes run in class w;
-# class 4 is the 512-lane, 19,712-slot table), "hub" (GSP_TEST_PV_DRAIN_LDS=300: every long row
-# in the hub kernel)
-CLASSES = ["h0", "h1", "h2", "h3", "h4", "hub"]
+# the drain kernels' row classes (pv_drain_class): "c0" as sized (class 0: <= 3,072 tuples,
+# 192 lanes), "c1" .. "c3" (GSP_TEST_PV_DRAIN_WIDE=1..3: the rows of the smaller classes run in
+# class w -- 256, 512 or 1024 lanes), "hub" (GSP_TEST_PV_DRAIN_LDS=300: every long row in the
+# hub kernel)
+CLASSES = ["c0", "c1", "c2", "c3", "hub"]
 
 
 def _set_class(monkeypatch, cls):
-    if cls.startswith("h") and cls != "hub" and cls != "h0":
+    if cls in ("c1", "c2", "c3"):
         monkeypatch.setenv("GSP_TEST_PV_DRAIN_WIDE", cls[1:])
     elif cls == "hub":
         monkeypatch.setenv("GSP_TEST_PV_DRAIN_LDS", "300")
 
 
-@pytest.mark.parametrize("cls", CLASSES[:5])
+@pytest.mark.parametrize("cls", CLASSES[:4])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "n%d_v%d_f%d" % c[:3])
 def test_drain_all_matches_oracle(case, cls, monkeypatch):
     _set_class(monkeypatch, cls)
@@ -134,13 +134,13 @@ EXT_CASES = [
 ]
 
 
-@pytest.mark.parametrize("cls", ["h0", "h4", "hub"])
+@pytest.mark.parametrize("cls", ["c0", "c3", "hub"])
 @pytest.mark.parametrize("case", EXT_CASES, ids=lambda c: "n%d_v%d_f%d_%s_g%d_tf%d_sw%d" % (
     c[0], c[1], c[2], "pol" if c[4] else "plain", c[5], c[6], c[7]))
 def test_drain_all_protocol_extensions(case, cls, monkeypatch):
     """TFAIL (a payload holds what the sender gossiped at t - 1), SWIM (the probe of t - 1
     answered or not before TREMOVE) and the JOINREP's bounded introducer list, every message
-    merged: GPU = oracle in the hash classes and the hub kernel, with events."""
+    merged: GPU = oracle in the LDS classes and the hub kernel, with events."""
     _set_class(monkeypatch, cls)
     monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
     n, V, f, drop, pol, shards, tfail, swim, ticks = case
@@ -165,7 +165,7 @@ def test_drain_all_kernel_forms(monkeypatch, form):
 
 def test_drain_all_hbm_paths(monkeypatch):
     """GSP_TEST_PV_DRAIN_LDS=300: every long row (more than 300 ids) is sorted and folded in
-    the hub kernel's HBM buffers instead of an LDS hash table."""
+    the hub kernel's HBM buffers instead of LDS."""
     _set_class(monkeypatch, "hub")
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=10, fail_mode=1, fail_tick=5, fail_ppm=20000, seed=31)
     _run(3000, 16, kw, every=4)
@@ -208,3 +208,135 @@ def test_drain_all_rejects_n_past_the_hub_buffers():
     from gossip_protocol_amd._lib import GspError
     with pytest.raises(GspError, match="drain all"):
         PviewEngine((1 << 21) - 700, view=32, inbox=0, max_ticks=2)
+
+
+# ---- BASELINE config 5 at its real size, drained ------------------------
+PV_FULL = dict(view=256, fanout=3, inbox=0, drop_pct=10, fail_mode=2, fail_tick=10,
+               fail_ppm=50000, seed=0x5EED)
+
+
+def _full_dead(n, seed=0x5EED, ftick=10, ppm=50000):
+    """the crashed block of config 5, from the oracle's Philox (oracle/pview_oracle.c)"""
+    from tests.oracle_binding import load_oracle
+    start = load_oracle().gsp_oracle_draw(0x4641494C, seed, ftick, 0xFFFFFFFF, 0, 0) % n
+    m = n * ppm // 1000000
+    dead = np.zeros(n, bool)
+    dead[(start + np.arange(m)) % n] = True
+    return dead, m
+
+
+def _view_abs(eng, x, t):
+    """(ids, hb, absolute ts) of x's view at tick t: every entry of a view at t has t - ts <
+    TREMOVE <= 31, so ts mod 32 names it; checks the view's form on the way"""
+    buf, ln = eng.row(x)
+    ids, hb, ts5 = unpack_view(buf, ln)
+    assert ln <= 256 and np.all(np.diff(ids) > 0) and x not in ids, "row %d" % x
+    assert np.all(buf[ln:] == np.uint64(0xFFFFFFFFFFFFFFFF))
+    return ids, hb, t - ((t - ts5) & 31)
+
+
+def _recompute_rows(eng, cfg, msgs, t, targets):
+    """Rows `targets` of tick t recomputed on the host from the views of t - 1 and the message
+    list sent at t - 1 (oracle/pview_oracle.c gsp_pview_oracle_row_step with inbox 0: every
+    message merged in ascending sender order, MP1Node.cpp:200-256, then TREMOVE :339-348 and
+    the bounded view's eviction), against the device's rows after tick t."""
+    from tests.oracle_binding import pview_row_step
+    senders = {}
+    hit = np.zeros(msgs.shape[0], bool)
+    for r in targets:
+        np.equal(msgs, r).any(axis=1, out=hit)
+        senders[r] = np.nonzero(hit)[0].tolist()
+    prev = {x: _view_abs(eng, x, t - 1) for x in set(targets) | {s for v in senders.values() for s in v}}
+    eng.step(1)
+    for r in targets:
+        (ids, hb, ts), _ = pview_row_step(cfg, t, r, prev[r], senders[r], [prev[s] for s in senders[r]])
+        gi, gh, gt = _view_abs(eng, r, t)
+        k = len(senders[r])
+        assert np.array_equal(gi, ids), "tick %d: ids of row %d (%d senders)" % (t, r, k)
+        assert np.array_equal(gh, hb), "tick %d: hb of row %d (%d senders)" % (t, r, k)
+        assert np.array_equal(gt, ts), "tick %d: ts of row %d (%d senders)" % (t, r, k)
+    return {r: len(senders[r]) for r in targets}
+
+
+def test_drain_all_full_size_rows_recomputed():
+    """Config 5 drained at its real size on one GPU (1,048,576 nodes, V = 256, fanout 3, 10 %
+    drop, 5 % contiguous crash at t = 10), ticks 1-14: every tick's node-rounds, delivered =
+    every message sent to an alive receiver (nothing overflows), sampled views well formed, and
+    from tick 6 on, rows recomputed on the host (_recompute_rows) -- every tick the receiver
+    with the most senders (a hub-class or class-3 row) and receivers sent 0, 3 (the split
+    kernels), 8-10, 11-14, 15-30 and 31-62 messages (LDS classes 0-3) when there are any."""
+    from tests.oracle_binding import PviewCfg
+    n, ticks = 1 << 20, 14
+    cfg = PviewCfg(n, 256, 3, 0, 10, 20, 1, 2, 10, 50000, 0x5EED)
+    dead, m = _full_dead(n)
+    rng = np.random.default_rng(11)
+    bands = [(0, 0), (3, 3), (8, 10), (11, 14), (15, 30), (31, 62)]
+    seen = set()
+    with PviewEngine(n, max_ticks=ticks, **PV_FULL) as eng:
+        eng.step(5)
+        for t in range(6, ticks + 1):
+            msgs = eng.messages()                        # sent at t - 1, merged at t
+            live = msgs[msgs >= 0]
+            cnt = np.bincount(live, minlength=n)
+            alive = ~dead if t > 10 else np.ones(n, bool)
+            rows = np.nonzero(alive)[0]
+            targets = [int(rows[np.argmax(cnt[rows])])]
+            for lo, hi in bands:
+                cand = rows[(cnt[rows] >= lo) & (cnt[rows] <= hi)]
+                if len(cand):
+                    targets.append(int(cand[rng.integers(len(cand))]))
+            ks = _recompute_rows(eng, cfg, msgs, t, targets)
+            seen |= set(ks.values())
+            d = eng.digest(t)
+            assert d["node_rounds"] == (n if t <= 10 else n - m), t
+            assert d["overflow"] == 0 and d["delivered"] == int(cnt[alive].sum()), t
+            for x in rng.integers(0, n, 32).tolist():
+                _view_abs(eng, x, t)
+    assert max(seen) > 62, "no hub-class row was recomputed (largest %d senders)" % max(seen)
+
+
+def test_drain_all_eight_row_shards_full_size():
+    """Config 5 drained at full size as 8 row shards in one process (the multi-GPU layout's
+    exchange with device copies in place of RCCL): every tick's digest, the message lists and
+    sampled views equal the one-shard engine's over 12 ticks."""
+    n, ticks, G = 1 << 20, 12, 8
+    rng = np.random.default_rng(9)
+    sample = sorted(set(rng.integers(0, n, 300).tolist()) | {0, 1, n - 1, n // G, n // G - 1})
+    with PviewEngine(n, max_ticks=ticks, **PV_FULL) as one:
+        want, msgs = [], []
+        for t in range(1, ticks + 1):
+            one.step(1)
+            want.append(one.digest(t))
+            msgs.append(one.messages())
+        rows = {r: one.row(r) for r in sample}
+    with PviewEngine(n, max_ticks=ticks, group=G, **PV_FULL) as eng:
+        for t in range(1, ticks + 1):
+            eng.step(1)
+            assert eng.digest(t) == want[t - 1], "tick %d" % t
+            assert np.array_equal(eng.messages(), msgs[t - 1]), "messages of tick %d" % t
+        for r in sample:
+            buf, ln = eng.row(r)
+            assert ln == rows[r][1] and np.array_equal(buf, rows[r][0]), "row %d" % r
+
+
+def test_drain_all_full_size_hub_past_1000_senders():
+    """Config 5 drained long enough that a receiver is sent more than 1,000 messages in one tick
+    (the bounded view's rich-get-richer hubs): that hub's row is recomputed on the
+    host -- the hub kernel's chunked HBM path at its real size."""
+    from tests.oracle_binding import PviewCfg
+    n, ticks = 1 << 20, 90
+    cfg = PviewCfg(n, 256, 3, 0, 10, 20, 1, 2, 10, 50000, 0x5EED)
+    dead, _ = _full_dead(n)
+    with PviewEngine(n, max_ticks=ticks, **PV_FULL) as eng:
+        eng.step(40)
+        for t in range(41, ticks + 1):
+            msgs = eng.messages()
+            cnt = np.bincount(msgs[msgs >= 0], minlength=n)
+            cnt[dead] = 0
+            hub = int(np.argmax(cnt))
+            if cnt[hub] > 1000:
+                ks = _recompute_rows(eng, cfg, msgs, t, [hub])
+                assert ks[hub] > 1000
+                return
+            eng.step(1)
+    pytest.fail("no receiver was sent more than 1,000 messages by tick %d" % ticks)
