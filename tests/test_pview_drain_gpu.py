@@ -263,7 +263,7 @@ def test_drain_all_full_size_rows_recomputed():
     drop, 5 % contiguous crash at t = 10), ticks 1-14: every tick's node-rounds, delivered =
     every message sent to an alive receiver (nothing overflows), sampled views well formed, and
     from tick 6 on, rows recomputed on the host (_recompute_rows) -- every tick the receiver
-    with the most senders (a hub-class or class-3 row) and receivers sent 0, 3 (the split
+    with the most senders (a class-3 row by tick 14) and receivers sent 0, 3 (the split
     kernels), 8-10, 11-14, 15-30 and 31-62 messages (LDS classes 0-3) when there are any."""
     from tests.oracle_binding import PviewCfg
     n, ticks = 1 << 20, 14
@@ -292,7 +292,9 @@ def test_drain_all_full_size_rows_recomputed():
             assert d["overflow"] == 0 and d["delivered"] == int(cnt[alive].sum()), t
             for x in rng.integers(0, n, 32).tolist():
                 _view_abs(eng, x, t)
-    assert max(seen) > 62, "no hub-class row was recomputed (largest %d senders)" % max(seen)
+    # by tick 14 the largest receivers are class-3 rows (31-62 senders); hubs past the LDS
+    # classes come later (test_drain_all_full_size_hub_past_1000_senders)
+    assert max(seen) > 30, "no class-3 row was recomputed (largest %d senders)" % max(seen)
 
 
 def test_drain_all_eight_row_shards_full_size():
