@@ -23,7 +23,9 @@ scaling); reports its own node-rounds/s, tick-kernel roofline, the drain row cla
 messages and kernel time (`drain_classes`), xGMI bytes per tick and the share of removals
 that hit live nodes (removes_of_live_frac, from the event run).  `pview_inbox7`: the same
 workload with the bounded inbox (at most 7 messages merged per receiver and tick; the share
-of delivered messages it discards is inbox_overflow_frac).
+of delivered messages it discards is inbox_overflow_frac).  `pview_swim`: the drain-all
+workload with SWIM probing and TFAIL (detection latency of the t = 10 crashes, removals of live
+members, kernel time against the plain run).
 Prints ONE JSON line (rank 0) with the roofline of the fused tick kernel and the CPU
 baseline (the oracle restatement, timed on a bounded sample of the same workload).
 """
@@ -193,17 +195,19 @@ def pview_cpu_baseline(budget_s=10.0, inbox=0):
 
 
 def run_pview(nodes, steps, warmup, world, local, dist, cpu_baseline_on, group=1, events=0,
-              inbox=None):
+              inbox=None, extra=None):
     """Config 5 on `world` GPUs (row shards).  Returns the rank-0 summary (None elsewhere).
     Algorithmic bytes per node-round: own view read + write (2 * V * 8) + one sender view per
     merged message (V * 8) + 4 B per CSR entry.  events: a kind mask (gsp_pview_params.events);
     the summary is then the event one (event_summary) with the kernel time.  inbox: 0 runs the
-    drain-all protocol (every message merged, gsp_pview_params.inbox = 0)."""
+    drain-all protocol (every message merged, gsp_pview_params.inbox = 0).  extra: more
+    gsp_pview_params fields (the protocol variants: tfail, swim)."""
     import torch
     from gossip_protocol_amd.pview import PviewEngine
     kw = dict(PV_KW, max_ticks=warmup + steps)
     if inbox is not None:
         kw["inbox"] = inbox
+    kw.update(extra or {})
     if events:
         kw.update(events=events, event_cap=EVENT_CAP)
     if dist is not None:
@@ -592,6 +596,8 @@ def main(argv=None):
                     help="skip the full-view row-layout line items (N > 1)")
     ap.add_argument("--no-events-off", action="store_true",
                     help="skip the events-off run of the headline workload")
+    ap.add_argument("--no-swim", action="store_true",
+                    help="skip the SWIM + TFAIL config-5 line item")
     ap.add_argument("--no-inbox7", action="store_true",
                     help="skip the bounded-inbox config-5 line item (inbox 7)")
     args = ap.parse_args(argv)
@@ -683,6 +689,25 @@ def main(argv=None):
         return r
     if not args.no_pview and not args.no_events:
         item("pview", lambda: _pv_events("pview"), "events")
+    def _pv_swim():
+        # config 5 drained with SWIM ping/ack probing (swim = 2: the direct ping and one
+        # indirect ping-req path) and TFAIL = 5 (a member 5 ticks stale is not gossiped): the
+        # crashes of t = 10 are found by probes within ticks instead of by TREMOVE at t = 30;
+        # a probe that loses both paths to the 10 % drop removes a live member
+        # (removes_of_live_frac).  Removal records on, as the pview events run.
+        r = run_pview(args.pview_nodes, min(args.steps, 30), args.warmup, world, local, dist,
+                      False, events=4, extra=dict(swim=2, tfail=5))
+        if r is None:
+            return None
+        r["protocol"] = "swim=2, tfail=5, inbox 0 (drain all), removal records on"
+        r["removes_of_live_frac"] = r["removes_of_live_nodes"] / r["removes"] if r["removes"] else 0.0
+        pe = out.get("pview", {}).get("events") if out is not None else None
+        if isinstance(pe, dict) and pe.get("kernel_ms"):
+            r["kernel_ms_plain"] = pe["kernel_ms"]
+            r["kernel_overhead_frac"] = r["kernel_ms"] / pe["kernel_ms"] - 1.0
+        return r
+    if not args.no_pview and not args.no_events and not args.no_swim:
+        item("pview_swim", _pv_swim)
     if not args.no_pview and not args.no_inbox7:
         # config 5 with the bounded inbox (at most 7 messages merged per receiver and tick):
         # the protocol of rounds 1-5's headline, beside the drain-all one

@@ -884,40 +884,172 @@ __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a
 
 // ---- LDS classes: one row's tuples in one LDS buffer, merged and folded in place ----------
 
-// One row of an LDS class, every message in one pass.
+// An LDS row's inputs, fetched while the row before it runs (the persistent loop below): the
+// chain list -> CSR offsets -> senders -> payload rows is three dependent HBM round trips,
+// so the first two links and the own view are read one row ahead.
+struct DIn {
+    int32_t lr, o0, k;                          // lr < 0: no row
+    bool dead;                                  // crashed, not started, or the job stopped
+    int32_t s, sl;                              // lane t < k: CSR entry t (sender, its row)
+    uint64_t own[2];                            // own-view slots (d_own's lane mapping)
+};
+
+__device__ __forceinline__ void d_fetch_row(const PviewTickArgs &a, DIn &in) {
+    in.k = 0;
+    in.o0 = 0;
+    in.dead = true;
+    if (in.lr < 0) return;
+    const int32_t r = a.row0 + in.lr;
+    in.o0 = a.csr_off[in.lr];
+    in.k = a.csr_off[in.lr + 1] - in.o0;                          // <= kDrainStage (the class)
+    in.dead = a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) || *a.err;
+}
+
+template <int NT>
+__device__ __forceinline__ void d_fetch_senders(const PviewTickArgs &a, DIn &in) {
+    const int32_t tid = threadIdx.x, V = a.view;
+    const int32_t per = V > NT ? 2 : 1;                          // V <= 256 <= 2 NT: contiguous slots
+    in.s = in.sl = 0;
+    in.own[0] = in.own[1] = kPvEmpty;
+    if (in.lr < 0 || in.dead) return;
+    if (tid < in.k) {
+        in.s = a.csr_src[in.o0 + tid];
+        in.sl = a.csr_slot ? a.csr_slot[in.o0 + tid] : in.s - a.row0;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int32_t i = tid * per + q;
+        if (q < per && i < V) in.own[q] = a.prev[int64_t(in.lr) * V + i];
+    }
+}
+
+// Step 1 of an LDS row: lane t < k ranks its sender against all k (distinct keys, broadcast LDS
+// reads; a JOINREP, sender kJoinRepSrc = -1, first: its sender is node 0) and writes the
+// sender's staging word at its rank.
+template <int NT>
+__device__ __forceinline__ void d_rank_stage(const PviewTickArgs &a, const DIn &in, uint32_t *keys, uint64_t *stage) {
+    const int32_t t = threadIdx.x;
+    const uint32_t key = uint32_t(in.s + 1);
+    if (t < in.k) keys[t] = key;
+    d_sync_lds();
+    if (t < in.k) {
+        int32_t rank = 0;
+        for (int32_t j = 0; j < in.k; ++j) rank += keys[j] < key ? 1 : 0;
+        stage[rank] = in.s == kJoinRepSrc ? kStageJoinRep
+                      : (uint64_t(uint32_t(in.s)) << 40) |
+                            (in.sl >= 0 ? uint64_t(in.sl) : (kStageRemote | uint64_t(-int64_t(in.sl) - 1)));
+    }
+    d_sync_lds();
+}
+
+// The list's first form from the fetched own view (d_own).
+template <int NT, class Sh, class P>
+__device__ __forceinline__ int32_t d_own_fetched(Sh &sh, P X, const DIn &in, uint32_t r) {
+    uint64_t e[2];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        e[q] = in.own[q];
+        const uint32_t x = uint32_t(e[q] >> 32), v = uint32_t(e[q]) & 0xFFFFu;
+        if (!(e[q] != kPvEmpty && x != r && v != 0u)) e[q] = kPvEmpty;
+        cnt += e[q] != kPvEmpty ? 1u : 0u;
+    }
+    uint32_t tot = 0;
+    uint32_t pos = d_scan<NT>(cnt, &tot, sh.red[1]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        if (e[q] != kPvEmpty) X[pos++] = d_tuple(uint32_t(e[q] >> 32), 0u, 1u, uint32_t(e[q]) & 0xFFFFu);
+    return int32_t(tot);
+}
+
+// Step 2 of an LDS row (d_build for one chunk of every message): the lane's E >= its tuples
+// payload loads all issued before the first is used -- one HBM round trip per row.
+template <int NT, int E, class P>
+__device__ __forceinline__ uint32_t d_build_lds(const PviewTickArgs &a, P X, const uint64_t *Y, int32_t L,
+                                                int32_t k, int32_t Vp, int32_t lgV, uint32_t r, const uint32_t *jm) {
+    const int32_t tid = threadIdx.x, V = a.view;
+    const uint32_t tf = uint32_t(a.tfail), t5m1 = (uint32_t(a.tick) - 1u) & 31u;
+    for (int32_t i = L + tid; i < Vp; i += NT) X[i] = kNone;
+    const int32_t np = k << lgV;                                 // payload tuples
+    const int32_t nt = np + ((k + Vp - 1) >> lgV << lgV);        // + the senders' run(s)
+    uint64_t e[E];
+    uint32_t cut = 0;                                            // bit u: slot not carried
+#pragma unroll
+    for (int u = 0; u < E; ++u) {
+        const int32_t q = u * NT + tid;
+        e[u] = kPvEmpty;
+        if (q < np) {
+            const int32_t m = q >> lgV, pos = q & (Vp - 1);
+            const uint64_t w = Y[m];
+            if (pos < V && !(w & kStageJoinRep)) {
+                const int64_t row = int64_t(w & kStageRow);
+                const uint64_t *p = (w & kStageRemote) ? a.remote : a.prev;
+                e[u] = p[row * V + pos];
+            } else if (pos < V && jm) {
+                e[u] = a.intro[pos];                             // the introducer list
+                cut |= ((jm[pos >> 5] >> (pos & 31)) & 1u) ? 0u : 1u << u;
+            }
+        } else if (q < nt && q - np < k) {
+            e[u] = Y[q - np];                                    // the staging word
+        }
+    }
+    uint32_t merged = 0;
+#pragma unroll
+    for (int u = 0; u < E; ++u) {
+        const int32_t q = u * NT + tid;
+        if (q >= nt) continue;
+        uint64_t key = kNone;
+        if (q < np) {
+            if (e[u] != kPvEmpty) {                              // a slot not carried: a no-op tuple
+                const bool carried = !((cut >> u) & 1u) && pv_gossiped(e[u], tf, t5m1);
+                merged += carried ? 1u : 0u;
+                const uint32_t x = uint32_t(e[u] >> 32), v = uint32_t(e[u]) & 0xFFFFu;
+                key = d_tuple(x, uint32_t(q >> lgV) + 1u, 0u, (x == r || !carried) ? 0u : v);
+            }
+        } else if (q - np < k) {
+            const uint32_t s = (e[u] & kStageJoinRep) ? 0u : uint32_t(e[u] >> 40);
+            key = d_tuple(s, uint32_t(q - np) + 1u, 1u, 0u);
+        }
+        X[Vp + q] = key;
+    }
+    __syncthreads();
+    return merged;
+}
+
+// One row of an LDS class, every message in one pass; nxt's inputs fetched on the way.
 template <bool kEv, int NT, int CAP>
-__device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, int32_t lr, int32_t it) {
+__device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, const DIn &cur,
+                                          DIn &nxt, int32_t it) {
     constexpr int E = CAP / NT;
-    const int32_t tid = threadIdx.x;
+    const int32_t tid = threadIdx.x, lr = cur.lr, k = cur.k;
     const uint32_t r = uint32_t(a.row0 + lr);
     if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);       // tests: each row exactly once
-    // crashed, not started yet, or the job stopped
-    if (a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) || *a.err) {
+    if (cur.dead) {                                              // crashed, not started, or stopped
         if (tid < 16) a.rowdig[int64_t(lr) * 16 + tid] = 0ull;
+        d_fetch_row(a, nxt);
+        d_fetch_senders<NT>(a, nxt);
         return;
     }
     const int32_t V = a.view;
     const uint32_t t5 = uint32_t(a.tick) & 31u, tr = uint32_t(a.tremove);
-    const int32_t o0 = a.csr_off[lr];
-    const int32_t k = a.csr_off[lr + 1] - o0;                    // <= kDrainStage (the class)
-    int32_t *src = a.csr_src + o0;
-    int32_t *slot = a.csr_slot ? a.csr_slot + o0 : nullptr;
     DMark pm;
     pm.init(a.prof, it, k);
-    d_rank_segment<NT>(src, slot, k, a.row0, sh.buf);            // 1. ascending senders
+    d_rank_stage<NT>(a, cur, reinterpret_cast<uint32_t *>(sh.buf), sh.stage);   // 1. ascending senders
+    d_fetch_row(a, nxt);
     uint32_t pcol;
     bool pok;
     pv_swim_probe(a, lr, r, pcol, pok);
-    const bool jpay = k > 0 && a.intro_list > 0 && src[0] == kJoinRepSrc;   // block-uniform
+    const bool jpay = k > 0 && a.intro_list > 0 && (sh.stage[0] & kStageJoinRep);   // block-uniform
     if (jpay) d_intro_mask<NT>(a, r, sh.jm, sh.red[1]);
     pm.mark(0);
     int32_t lgV = 0;
     while ((1 << lgV) < V) ++lgV;
     const int32_t Vp = 1 << lgV;
     const SkewBuf X{sh.buf};
-    const int32_t L0 = d_own<NT>(a, sh, X, lr, r);               // <= V: padded to Vp
+    const int32_t L0 = d_own_fetched<NT>(sh, X, cur, r);         // <= V: padded to Vp
     pm.mark(1);
-    const uint32_t merged = d_build<NT>(a, X, sh.stage, L0, Vp, 0, k, Vp, lgV, src, slot, r, jpay ? sh.jm : nullptr);
+    const uint32_t merged = d_build_lds<NT, E>(a, X, sh.stage, L0, k, Vp, lgV, r, jpay ? sh.jm : nullptr);
+    d_fetch_senders<NT>(a, nxt);                                 // in flight through steps 3-6
     pm.mark(2);
     const int32_t N = Vp + (k << lgV) + ((k + Vp - 1) >> lgV << lgV);
     d_merge_ip<NT, E>(X, N, Vp);
@@ -935,9 +1067,18 @@ __global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a)
     __shared__ DrainShared<NT, CAP> sh;
     const int32_t cnt = a.long_list[kCls];
     const int32_t *list = a.long_list + kDrainHead + int64_t(kCls) * a.rows;
-    for (int32_t i = int32_t(blockIdx.x); i < cnt; i += int32_t(gridDim.x)) {
-        d_row_lds<kEv, NT, CAP>(a, sh, list[i], (i - int32_t(blockIdx.x)) / int32_t(gridDim.x));
+    const int32_t step = int32_t(gridDim.x);
+    int32_t i = int32_t(blockIdx.x);
+    if (i >= cnt) return;
+    DIn cur, nxt;
+    cur.lr = list[i];
+    d_fetch_row(a, cur);
+    d_fetch_senders<NT>(a, cur);
+    for (; i < cnt; i += step) {
+        nxt.lr = i + step < cnt ? list[i + step] : -1;
+        d_row_lds<kEv, NT, CAP>(a, sh, cur, nxt, (i - int32_t(blockIdx.x)) / step);
         d_sync_lds();                                            // LDS free for the next row
+        cur = nxt;
     }
 }
 

@@ -151,6 +151,10 @@ def test_bench_two_ranks_gloo():
     pe = pv["events"]                                 # the partial view's removes-only run
     assert "error" not in pe, pe
     assert pe["kinds"] == 4 and pe["crashed_nodes_detected"] == 2 and pe["kernel_overhead_frac"] == 0.0
+    ps = d["pview_swim"]                              # SWIM + TFAIL drained, removal records
+    assert "error" not in ps, ps
+    assert ps["protocol"].startswith("swim=2, tfail=5") and ps["kernel_overhead_frac"] == 0.0
+    assert ps["removes_of_live_frac"] == 0.0 and ps["crashed_nodes_detected"] == 2
 
 
 INBOXES_WITH_PMC = [7]        # committed profiles/pmc_*_pview*.json (0: drain all, 7: inbox 7)
