@@ -47,7 +47,7 @@ def main():
                "read_bytes_per_tick": rd, "write_bytes_per_tick": wr, "bytes_per_tick": rd + wr,
                "bytes_per_launch": (rd + wr) / max(1, launches),
                "correction": "FETCH_SIZE x2 (gfx950 counts half of 16-B/lane streaming reads)",
-               "source": "profiles/r05/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each, "
+               "source": "profiles/r06/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each, "
                          "scripts/pmc_c3.sh)" % tag},
               open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
     print("launches/tick %d bytes/tick %.4g" % (launches, rd + wr))

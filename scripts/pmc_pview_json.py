@@ -51,7 +51,7 @@ def main():
     tag = os.path.basename(os.path.normpath(src))
     counters = {c: {"per_launch": v, "per_tick": v, "ticks": list(TICKS)} for c, v in sorted(sq.items())}
     json.dump({"kernel": "pview tick kernels (%s), per tick" % what, "window_ticks": list(TICKS),
-               "source": "gpurun_out/%s (rocprofv3 --pmc, scripts/pmc_pview.sh + pmc_pview_json.py)" % tag,
+               "source": "profiles/r06/%s (rocprofv3 --pmc, scripts/pmc_pview.sh + pmc_pview_json.py)" % tag,
                "counters": counters}, open(os.path.join(dst, "pmc_sq_pview%s.json" % suffix), "w"), indent=1)
     fetch = per_tick(os.path.join(src, "pmc_fetch"))["FETCH_SIZE"]
     write = per_tick(os.path.join(src, "pmc_write"))["WRITE_SIZE"]
@@ -63,7 +63,7 @@ def main():
                "bytes_per_launch": rd + wr,
                "correction": "FETCH_SIZE x2 (the gfx950 16-B/lane rule applied to this kernel's 8-B/lane view "
                              "loads: uncalibrated for that width, MI355X_MICROARCH.md HBM section)",
-               "source": "gpurun_out/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each)" % tag},
+               "source": "profiles/r06/%s (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one pass each)" % tag},
               open(os.path.join(dst, "pmc_traffic_pview%s.json" % suffix), "w"), indent=1)
     print("VALU/tick %.4g SALU/tick %.4g bytes/tick %.4g" % (sq["SQ_INSTS_VALU"], sq["SQ_INSTS_SALU"], rd + wr))
 

@@ -157,7 +157,7 @@ def test_bench_two_ranks_gloo():
     assert ps["removes_of_live_frac"] == 0.0 and ps["crashed_nodes_detected"] == 2
 
 
-INBOXES_WITH_PMC = [7]        # committed profiles/pmc_*_pview*.json (0: drain all, 7: inbox 7)
+INBOXES_WITH_PMC = [0, 7]       # committed profiles/pmc_*_pview*.json (0: drain all, 7: inbox 7)
 
 
 def test_counter_fields_only_for_their_window():
