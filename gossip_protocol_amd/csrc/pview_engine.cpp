@@ -93,6 +93,10 @@ struct gsp_pview {
     int32_t drain_wide = 0;      // tests: GSP_TEST_PV_DRAIN_WIDE=w runs the rows of classes < w in class w
     int32_t *h_err = nullptr;    // pinned mirror of the shards' capacity flags (async copies)
     int32_t *h_dhead = nullptr;  // drain all: pinned copy of a shard's long_list head (class sizes)
+    bool nowait = false;         // row shards: no host wait for the bucket sizes (PviewTickArgs.nowait;
+                                 // GSP_TEST_PV_NOWAIT=0/1 turns it off / on for tests)
+    int32_t *h_dring = nullptr;  // nowait + drain all: pinned [max_ticks + 1][local shards][kDrainHead]
+    std::vector<std::pair<int32_t, int32_t>> dring_pending;   // (tick, local shard) heads to add
     // drain all: per class, rows and messages run and kernel ms (gsp_pview_drain_stats)
     using DrainEvents = std::array<hipEvent_t, gsp::kDrainClasses + 1>;
     std::vector<DrainEvents> dpending;
@@ -164,6 +168,7 @@ struct gsp_pview {
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
+        a.nowait = nowait ? 1 : 0;
         if (drain) {
             a.drain = 1;
             a.long_list = sh.long_list.p;
@@ -176,6 +181,8 @@ struct gsp_pview {
             a.drain_lds = drain_lds;
             a.drain_wide = drain_wide;
             a.drain_rows = h_dhead;
+            if (nowait && h_dring)
+                a.dhead_async = h_dring + (size_t(t) * local.size() + size_t(&sh - local.data())) * gsp::kDrainHead;
         }
         return a;
     }
@@ -432,6 +439,14 @@ int pview_collect(gsp_pview *s) {
         for (hipEvent_t e : de) s->free_events.push_back(e);
     }
     s->dpending.clear();
+    for (const auto &ti : s->dring_pending) {      // the stream has been synchronised
+        const int32_t *h = s->h_dring + (size_t(ti.first) * s->local.size() + size_t(ti.second)) * gsp::kDrainHead;
+        for (int c = 0; c < gsp::kDrainClasses; ++c) {
+            s->drain_rows[c] += h[c];
+            s->drain_msgs[c] += h[8 + c];
+        }
+    }
+    s->dring_pending.clear();
     if (s->rowmode)
         if (int rc = gsp::rowx_collect(s->rowx, &s->perf.xgmi_bytes)) return rc;
     for (size_t i = 0; i < s->local.size(); ++i)
@@ -463,6 +478,11 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
         GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
         if (p->inbox == 0) GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_dhead), gsp::kDrainHead * 4));
+        s->nowait = s->rowmode;
+        if (const char *nw = std::getenv("GSP_TEST_PV_NOWAIT")) s->nowait = std::atoi(nw) != 0;
+        if (s->nowait && p->inbox == 0)
+            GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_dring),
+                                  size_t(p->max_ticks + 1) * size_t(local_shards) * gsp::kDrainHead * 4));
     }
     GSP_HIP(hipDeviceGetAttribute(&s->cus, hipDeviceAttributeMultiprocessorCount, device));
     s->h_fail = gsp::fail_ticks(p->policy, p->n, p->seed, p->fail_mode, p->fail_tick, p->fail_ppm);
@@ -592,6 +612,7 @@ int gsp_pview_destroy(gsp_pview *s) {
     if (s->h_err) (void)hipHostFree(s->h_err);
     if (s->h_kcount) (void)hipHostFree(s->h_kcount);
     if (s->h_dhead) (void)hipHostFree(s->h_dhead);
+    if (s->h_dring) (void)hipHostFree(s->h_dring);
     if (s->kcount_ev) (void)hipEventDestroy(s->kcount_ev);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
@@ -652,7 +673,9 @@ int gsp_pview_step(gsp_pview *s, int32_t ticks) {
             }
             GSP_HIP(gsp::launch_pview_tick(ta, s->st));
             if (ta.drain_ev) s->dpending.push_back(de);
-            if (s->drain && s->h_dhead)          // the class sizes this launch read back
+            if (s->drain && ta.nowait && ta.dhead_async)   // copied without a wait: read after a sync
+                s->dring_pending.emplace_back(t, int32_t(&sh - s->local.data()));
+            else if (s->drain && s->h_dhead)     // the class sizes this launch read back
                 for (int c = 0; c < gsp::kDrainClasses; ++c) {
                     s->drain_rows[c] += s->h_dhead[c];
                     s->drain_msgs[c] += s->h_dhead[8 + c];

@@ -1002,6 +1002,10 @@ __global__ void __launch_bounds__(NT, kMinWaves) pview_tick_split_kernel(PviewTi
     constexpr int kKeys = NT == 64 ? 512 : kQhi <= 3 ? 1024 : (kQhi + 1) * kSlots;
     __shared__ std::conditional_t<kIP, PvSharedIP<kKeys>, PvShared<kKeys>> sh;
     static_assert(NT != 64 || kQhi <= 1, "one-wave rows hold at most 2 sources");
+    int32_t tot = 0;                             // the range's rows: a grid past them (a.nowait)
+#pragma unroll
+    for (int q = kQlo; q <= kQhi; ++q) tot += a.kcount[q];
+    if (int32_t(blockIdx.x) >= tot) return;
     pv_row<kExt, NT, kQlo, kQhi>(a, sh, pv_row_of<kQlo, kQhi>(a, int32_t(blockIdx.x)));
 }
 
@@ -1359,16 +1363,29 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         // (round 5: on one box, ticks 6-25, 5.36 ms against 5.42 for round 3's grids predicted
         // without a wait plus an overflow kernel, and 6.7-13 ms for persistent kernels pulling
         // row chunks from per-XCD heads -- DESIGN.md 4b)
-        if (!a.kcount_host || !a.kcount_event) return hipErrorInvalidValue;
+        // Row shards (a.nowait) skip that wait: every range launches on `rows` workgroups, those
+        // past the range's bucket exit after reading its counts (pview_tick_split_kernel), so
+        // the host queues tick after tick behind the exchange's collectives.
         PviewTickArgs b = a;
         int32_t c[8];
-        if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-            (a.drain && a.drain_rows &&
-             hipMemcpyAsync(a.drain_rows, a.long_list, kDrainHead * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-            hipEventRecord(a.kcount_event, st) != hipSuccess || hipEventSynchronize(a.kcount_event) != hipSuccess)
-            return hipGetLastError();
-        for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
-        const unsigned g67 = unsigned(c[6] + c[7]), g5 = unsigned(c[5]), g4 = unsigned(c[4]),
+        if (a.nowait) {
+            for (int q = 0; q < 8; ++q) c[q] = q == 0 ? a.rows : 0;
+            b.drain_rows = nullptr;
+            if (a.drain && a.dhead_async &&
+                hipMemcpyAsync(a.dhead_async, a.long_list, kDrainHead * 4, hipMemcpyDeviceToHost, st) != hipSuccess)
+                return hipGetLastError();
+        } else {
+            if (!a.kcount_host || !a.kcount_event) return hipErrorInvalidValue;
+            if (hipMemcpyAsync(a.kcount_host, a.kcount, 8 * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                (a.drain && a.drain_rows &&
+                 hipMemcpyAsync(a.drain_rows, a.long_list, kDrainHead * 4, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+                hipEventRecord(a.kcount_event, st) != hipSuccess || hipEventSynchronize(a.kcount_event) != hipSuccess)
+                return hipGetLastError();
+            for (int q = 0; q < 8; ++q) c[q] = a.kcount_host[q];
+        }
+        const unsigned g67 = a.nowait ? unsigned(a.rows) : unsigned(c[6] + c[7]),
+                       g5 = a.nowait ? unsigned(a.rows) : unsigned(c[5]),
+                       g4 = a.nowait ? unsigned(a.rows) : unsigned(c[4]),
                        g03 = unsigned(c[0] + c[1] + c[2] + c[3]);
         // k = 6, 7: 256-lane rows in 20 KB, 8 waves per SIMD (8 rows per CU); k = 5 / k = 4:
         // 128-lane rows merged in place (PvSharedIP, 11.3 / 9.8 KB) at 6 / 7 waves per SIMD (12 /

@@ -85,6 +85,11 @@ struct PviewTickArgs {
     int32_t *drain_rows;         // pinned [kDrainHead]: long_list's head, copied back with the
                                  // split kernels' bucket sizes -- the drain classes' grids (a
                                  // class without rows is not launched), or null (persistent grids)
+    int32_t nowait;              // 1 (row shards): no host wait for the bucket sizes -- every split
+                                 // kernel launches on `rows` workgroups (those past their bucket
+                                 // exit at once), the drain classes on persistent grids
+    int32_t *dhead_async;        // nowait + drain all: pinned [kDrainHead], long_list's head copied
+                                 // without a wait (the engine reads it after its next sync), or null
     hipEvent_t *drain_ev;        // [kDrainClasses + 1]: recorded before the first drain class and
                                  // after each (the per-class kernel time), or null
 };

@@ -181,6 +181,35 @@ def _run_case(case, h0=1, evict_order=0):
         _cmp_rows(eng, orc, range(n) if n <= 2000 else range(0, n, 7))
 
 
+# Row shards launch the split kernels without a host wait for the bucket sizes (PviewTickArgs.
+# nowait: every k range on `rows` workgroups, those past their bucket exit at once; the drain
+# classes on persistent grids; their sizes copied back without a wait). GSP_TEST_PV_NOWAIT=1
+# forces that form on one shard, =0 puts the exact grids back on an in-process group. Ticks are
+# queued four at a time, so the host runs ahead of the device.
+@pytest.mark.parametrize("inbox", [7, 0])
+@pytest.mark.parametrize("nowait,group", [("1", 1), ("0", 3)], ids=["nowait_g1", "exact_g3"])
+def test_pview_nowait_grids_match_oracle(inbox, nowait, group, monkeypatch):
+    monkeypatch.setenv("GSP_TEST_PV_NOWAIT", nowait)
+    monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
+    n, ticks = 2500, 16
+    kw = dict(view=32, fanout=8 if inbox == 0 else 3, inbox=inbox, drop_pct=10, fail_mode=1,
+              fail_tick=6, fail_ppm=30000, seed=23)
+    orc = PviewOracle(n, **kw)
+    with PviewEngine(n, max_ticks=ticks, group=group, **kw) as eng:
+        for t0 in range(0, ticks, 4):
+            want = [orc.step() for _ in range(4)]
+            eng.step(4)
+            for i, w in enumerate(want):
+                t = t0 + i + 1
+                assert eng.digest(t) == w, "tick %d" % t
+                assert eng.rows_run(t) == n, "tick %d: %d rows run" % (t, eng.rows_run(t))
+        eng._tick = ticks
+        _cmp_rows(eng, orc, range(0, n, 3))
+        if inbox == 0:                               # the class sizes reached the host
+            st = eng.drain_stats()
+            assert sum(st["rows"]) > 0 and sum(st["messages"]) >= 8 * sum(st["rows"])
+
+
 SHARD_CASES = [
     # n, view, fanout, inbox, drop, fail_mode, fail_tick, ppm, seed, ticks, shards
     (3000, 64, 3, 7, 10, 2, 6, 50000, 5, 20, 2),
