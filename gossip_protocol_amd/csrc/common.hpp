@@ -56,6 +56,23 @@ struct DevBuf {
         if (e == hipSuccess) n = count;
         return e;
     }
+    // physically contiguous device memory (hipDeviceMallocContiguous): the page-table fragments
+    // may then span the whole allocation; falls back to hipMalloc when the driver refuses
+    hipError_t alloc_contiguous(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void **>(&p), (count ? count : 1) * sizeof(T),
+                                             hipDeviceMallocContiguous);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+            return alloc(count);
+        }
+        n = count;
+        return e;
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;

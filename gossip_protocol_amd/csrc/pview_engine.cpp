@@ -77,7 +77,7 @@ struct gsp_pview {
     int64_t pair_cap = 0, msg_cap = 0;
     int32_t tick = 0;
     bool timing = true;
-    int32_t split = 1;           // GSP_PV_SPLIT=0: every row in the one 256-lane kernel; else
+    int32_t split = 1;           // GSP_TEST_PV_SPLIT=0: every row in the one 256-lane kernel; else
                                  // rows bucketed by k into four kernels (pview_kernels.hip)
     bool pos_scatter = false;    // one shard, no join schedule: the receiver CSR is scattered from
                                  // the positions the send kernel's deg atomics returned (the
@@ -86,7 +86,7 @@ struct gsp_pview {
     int32_t *h_kcount = nullptr; // pinned [8]: the bucket sizes, the split kernels' grids
     hipEvent_t kcount_ev = nullptr;
     int32_t max_segment = gsp::kPvMaxSegment;
-    bool sort_rows = true;       // run rows k-descending (GSP_PV_SORT=0 turns it off)
+    bool sort_rows = true;       // run rows k-descending (GSP_TEST_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
     int64_t scratch_cap = 0;     // HBM drain kernel: tuples per buffer (two per workgroup)
     int32_t drain_lds = gsp::kDrainLdsMax;   // drain kernels: LDS tuples (GSP_TEST_PV_DRAIN_LDS lowers it)
@@ -472,8 +472,8 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
     s->shards = shards;
     s->rank = rank;
     s->rowmode = shards > 1 || nccl_id != nullptr;
-    if (const char *sp = std::getenv("GSP_PV_SPLIT")) s->split = std::atoi(sp);
-    if (const char *so = std::getenv("GSP_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
+    if (const char *sp = std::getenv("GSP_TEST_PV_SPLIT")) s->split = std::atoi(sp);
+    if (const char *so = std::getenv("GSP_TEST_PV_SORT")) s->sort_rows = std::atoi(so) != 0;
     if (s->split && s->sort_rows) {
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
         GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
@@ -502,7 +502,7 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         if (const char *dw = std::getenv("GSP_TEST_PV_DRAIN_WIDE")) s->drain_wide = std::max(0, std::min(3, std::atoi(dw)));
     }
     s->pos_scatter = !s->rowmode && !s->joins;
-    if (const char *ps = std::getenv("GSP_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
+    if (const char *ps = std::getenv("GSP_TEST_PV_POS_SCATTER"); ps && !std::atoi(ps)) s->pos_scatter = false;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
     int32_t max_rows = 0;
     for (int32_t g = 0; g < shards; ++g)

@@ -9,7 +9,7 @@
 //   128-lane rows merged in place (one key buffer, 11.3 / 9.8 KB, PvSharedIP), k <= 3 as
 //   128-lane rows in 10 KB; k = 0 rows of the plain protocol skip steps 2-5 (pv_own_only).
 //   Each range's grid is its bucket size, read back behind an event after the receipt kernel.
-//   pview_tick_kernel is the one-kernel form (GSP_PV_SPLIT=0: one 256-lane workgroup per row,
+//   pview_tick_kernel is the one-kernel form (GSP_TEST_PV_SPLIT=0: one 256-lane workgroup per row,
 //   any k).  The row body:
 //   1. loads: the own view is requested first; the receipt record is read by every wave
 //      (no barrier) and the k sender views follow, one coalesced 2 KB row each;
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(kPvBlock) pview_init_kernel(PviewTickArgs a) {
     pv_finish<kPvBlock>(a, sh, lr, 0, 0, true, ro);
 }
 
-// The one-kernel form (GSP_PV_SPLIT=0; every row a 256-lane row in 20 KB, any k).  One row
+// The one-kernel form (GSP_TEST_PV_SPLIT=0; every row a 256-lane row in 20 KB, any k).  One row
 // per workgroup: a software-pipelined variant (the next row's record, own view and first
 // sender views requested while the current row merged, two rows per workgroup) measured 4-8 %
 // slower -- other resident rows already hide the HBM round trips.

@@ -83,7 +83,7 @@ struct gsp_scale {
     bool timing = true;
     int policy = 5;            // bit 0 nt own row, bit 1 nt sender rows, bit 2 pipelined loads
     int merge = 1;             // 1 packed 16-bit merge, 0 per-entry form
-    int32_t lds_pad = 0;       // GSP_SCALE_LDS_PAD: extra LDS per tick-kernel workgroup
+    int32_t lds_pad = 0;       // GSP_TEST_SCALE_LDS_PAD: extra LDS per tick-kernel workgroup
     std::vector<Shard> local;  // shards held by this engine (1, or G for an in-process group)
     gsp::DevBuf<gsp::ScaleTickArgs> long_tpl;   // [local][2]: every tile's args by tick parity
                                                 // (scale_long_kernel)
@@ -238,8 +238,11 @@ int shard_alloc(gsp_scale *s, Shard &sh) {
     const size_t rows = size_t(sh.rows);
     const size_t tab = rows * size_t(s->stride);
     hipStream_t st = s->st;
+    // tests / A/B (GSP_TEST_SCALE_CONTIG=1): the tables in physically contiguous memory
+    const char *contig = std::getenv("GSP_TEST_SCALE_CONTIG");
     for (int b = 0; b < 2; ++b) {
-        GSP_HIP(sh.table[b].alloc(tab));
+        if (contig && std::atoi(contig)) GSP_HIP(sh.table[b].alloc_contiguous(tab));
+        else GSP_HIP(sh.table[b].alloc(tab));
         GSP_HIP(sh.cnt_total[b].alloc(size_t(n)));
         GSP_HIP(hipMemsetAsync(sh.cnt_total[b].p, 0, size_t(n) * 4, st));
     }
@@ -570,7 +573,7 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
                     (layout == GSP_SHARD_COLUMNS && shards % local_shards == 0 && rank % local_shards == 0),
                 GSP_ERR_INVALID, "gsp_scale: %d local tiles of %d column shards at shard %d", local_shards,
                 shards, rank);
-    if (const char *sx = std::getenv("GSP_SCALE_SHARED")) s->shared = s->shared && std::atoi(sx) != 0;
+    if (const char *sx = std::getenv("GSP_TEST_SCALE_SHARED")) s->shared = s->shared && std::atoi(sx) != 0;
     s->rowmode = sharded && layout == GSP_SHARD_ROWS;
     const int64_t unit = int64_t(gsp::kChunk) * (s->sliced ? shards : 1);
     s->width = (int64_t(p->n) + unit - 1) / unit * unit;
@@ -590,9 +593,9 @@ int scale_build(const gsp_scale_params *p, int device, int32_t shards, int32_t r
     s->h_start = gsp::start_ticks(p->policy, p->n);
     s->joins = p->policy.step_rate > 0 && *std::max_element(s->h_start.begin(), s->h_start.end()) > 0;
     if (s->joins) s->plan = gsp::join_plan(s->h_start, p->max_ticks + 1);
-    if (const char *pol = std::getenv("GSP_SCALE_POLICY")) s->policy = std::atoi(pol) & 7;
-    if (const char *pad = std::getenv("GSP_SCALE_LDS_PAD")) s->lds_pad = std::max(0, std::min(65536, std::atoi(pad)));
-    if (const char *m = std::getenv("GSP_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
+    if (const char *pol = std::getenv("GSP_TEST_SCALE_POLICY")) s->policy = std::atoi(pol) & 7;
+    if (const char *pad = std::getenv("GSP_TEST_SCALE_LDS_PAD")) s->lds_pad = std::max(0, std::min(65536, std::atoi(pad)));
+    if (const char *m = std::getenv("GSP_TEST_SCALE_MERGE")) s->merge = std::atoi(m) ? 1 : 0;
     if (!s->sliced) {
         // the fused kernel keeps the row's presence bitmap (and the event stage) in LDS next
         // to 8.3 KB of statics

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Config-3 tick-kernel time under environment variants (GSP_LIB_VARIANT=<tag> of a
-`make lib-variant` library, GSP_SCALE_POLICY, ...), each in its own child process, interleaved:
-    python scripts/ab_scale_env.py base: nosend:GSP_LIB_VARIANT=nosend pol1:GSP_SCALE_POLICY=1
+`make lib-variant` library, GSP_TEST_SCALE_POLICY, ...), each in its own child process, interleaved:
+    python scripts/ab_scale_env.py base: nosend:GSP_LIB_VARIANT=nosend pol1:GSP_TEST_SCALE_POLICY=1
 """
 import json
 import os

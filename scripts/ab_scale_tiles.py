@@ -4,6 +4,8 @@ environment variants, each in its own child process, interleaved; per variant an
 tick kernels' ms per launch and per tick, and the CSR (+ segment order) ms per tick, over the
 driver's window (ticks 6-25).
     python scripts/ab_scale_tiles.py [reps] base: nopre:GSP_LIB_VARIANT=nopresort
+AB_N / AB_G / AB_W / AB_S (environment) change the nodes, tiles, warm-up and timed ticks
+(config 4 as bench.py runs it: AB_N=262144 AB_G=32 AB_W=2 AB_S=8).
 """
 import os
 import subprocess
@@ -14,14 +16,17 @@ CHILD = r'''
 import json, sys
 sys.path.insert(0, %r)
 from gossip_protocol_amd.scale import FAIL_RANDOM, ScaleEngine
-with ScaleEngine(65536, fanout=3, fail_mode=FAIL_RANDOM, fail_tick=10, fail_ppm=10000,
-                 seed=0x5EED, max_ticks=32, group=8) as e:
-    e.step(5); e.sync(); p0 = e.perf(); e.step(20); e.sync(); p1 = e.perf()
-    d = e.digest(25)
+import os
+N, G = int(os.environ.get("AB_N", 65536)), int(os.environ.get("AB_G", 8))
+W, S = int(os.environ.get("AB_W", 5)), int(os.environ.get("AB_S", 20))
+with ScaleEngine(N, fanout=3, fail_mode=FAIL_RANDOM, fail_tick=10, fail_ppm=10000,
+                 seed=0x5EED, max_ticks=W + S + 2, group=G) as e:
+    e.step(W); e.sync(); p0 = e.perf(); e.step(S); e.sync(); p1 = e.perf()
+    d = e.digest(W + S)
 launches = p1["merge_launches"] - p0["merge_launches"]
 ms = p1["merge_ms"] - p0["merge_ms"]
-print(json.dumps({"ms_per_launch": ms / launches, "kernel_ms_per_tick": ms / 20,
-                  "csr_ms_per_tick": (p1["csr_ms"] - p0["csr_ms"]) / 20,
+print(json.dumps({"ms_per_launch": ms / launches, "kernel_ms_per_tick": ms / S,
+                  "csr_ms_per_tick": (p1["csr_ms"] - p0["csr_ms"]) / S,
                   "hash": d["event_hash"] if isinstance(d, dict) else None}))
 ''' % ROOT
 
@@ -36,6 +41,6 @@ if __name__ == "__main__":
                 k, _, v = kv.partition("=")
                 env[k] = v
             r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
-                               timeout=240)
+                               timeout=int(os.environ.get("AB_TIMEOUT", 240)))
             out = r.stdout.strip().splitlines()
             print(name, out[-1] if out else r.stderr[-600:], flush=True)

@@ -153,11 +153,11 @@ def test_drain_all_protocol_extensions(case, cls, monkeypatch):
 
 @pytest.mark.parametrize("form", ["0:1", "1:1", "0:0"])
 def test_drain_all_kernel_forms(monkeypatch, form):
-    """The one-kernel form (GSP_PV_SPLIT=0) with and without row order (GSP_PV_SORT): a long
+    """The one-kernel form (GSP_TEST_PV_SPLIT=0) with and without row order (GSP_TEST_PV_SORT): a long
     row reaches pview_tick_kernel there and must be left to the drain kernel."""
     split, sort = form.split(":")
-    monkeypatch.setenv("GSP_PV_SPLIT", split)
-    monkeypatch.setenv("GSP_PV_SORT", sort)
+    monkeypatch.setenv("GSP_TEST_PV_SPLIT", split)
+    monkeypatch.setenv("GSP_TEST_PV_SORT", sort)
     monkeypatch.setenv("GSP_TEST_PV_COUNT_ROWS", "1")
     kw = dict(view=32, fanout=8, inbox=0, drop_pct=0, fail_mode=2, fail_tick=5, fail_ppm=50000, seed=29)
     _run(2000, 14, kw, rows_run=True, every=7)

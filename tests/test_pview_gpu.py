@@ -57,15 +57,15 @@ def test_pview_eviction_bins_match_oracle(case):
     _run_case(case[:-1], h0=case[-1])
 
 
-# the tick kernel's launch forms -- GSP_PV_SPLIT: 0 one 256-lane kernel for every row, 1 rows
+# the tick kernel's launch forms -- GSP_TEST_PV_SPLIT: 0 one 256-lane kernel for every row, 1 rows
 # bucketed by k into four kernels on exact grids (the bucket sizes read back each tick; round 5
 # -- they replace round 3's predicted grids and overflow kernel); the second field 0 turns off
 # the one-shard receiver CSR scattered from the send kernel's returned slots
-# (GSP_PV_POS_SCATTER=0: the atomic fill-counter scatter instead)
+# (GSP_TEST_PV_POS_SCATTER=0: the atomic fill-counter scatter instead)
 def _set_form(monkeypatch, form):
     split, pos = (form.split(":") + ["1"])[:2]
-    monkeypatch.setenv("GSP_PV_SPLIT", split)
-    monkeypatch.setenv("GSP_PV_POS_SCATTER", pos)
+    monkeypatch.setenv("GSP_TEST_PV_SPLIT", split)
+    monkeypatch.setenv("GSP_TEST_PV_POS_SCATTER", pos)
 
 
 @pytest.mark.parametrize("form", ["0", "1", "1:0", "0:0"])
