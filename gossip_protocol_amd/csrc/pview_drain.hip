@@ -884,6 +884,8 @@ __global__ void __launch_bounds__(kHT, 1) pview_drain_hbm_kernel(PviewTickArgs a
 
 // ---- LDS classes: one row's tuples in one LDS buffer, merged and folded in place ----------
 
+constexpr int d_pow2_ceil(int x) { return x <= 1 ? 1 : 2 * d_pow2_ceil((x + 1) / 2); }
+
 // An LDS row's inputs, fetched while the row before it runs (the persistent loop below): the
 // chain list -> CSR offsets -> senders -> payload rows is three dependent HBM round trips,
 // so the first two links and the own view are read one row ahead.
@@ -1020,7 +1022,7 @@ __device__ __forceinline__ uint32_t d_build_lds(const PviewTickArgs &a, P X, con
 template <bool kEv, int NT, int CAP>
 __device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT, CAP> &sh, const DIn &cur,
                                           DIn &nxt, int32_t it) {
-    constexpr int E = CAP / NT;
+    constexpr int E = d_pow2_ceil((CAP + NT - 1) / NT);          // tuples per lane (a power of two)
     const int32_t tid = threadIdx.x, lr = cur.lr, k = cur.k;
     const uint32_t r = uint32_t(a.row0 + lr);
     if (a.rows_run && tid == 0) atomicAdd(a.rows_run, 1);       // tests: each row exactly once
@@ -1062,8 +1064,8 @@ __device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT
 
 // The rows of LDS class kCls: workgroup b takes rows b, b + grid, ... (a persistent grid of
 // rows-per-CU x CUs, or, with the host's copy of the class sizes, one row per workgroup)
-template <bool kEv, int NT, int CAP, int kCls>
-__global__ void __launch_bounds__(NT, 4) pview_drain_lds_kernel(PviewTickArgs a) {
+template <bool kEv, int NT, int CAP, int kCls, int kWaves = 4>
+__global__ void __launch_bounds__(NT, kWaves) pview_drain_lds_kernel(PviewTickArgs a) {
     __shared__ DrainShared<NT, CAP> sh;
     const int32_t cnt = a.long_list[kCls];
     const int32_t *list = a.long_list + kDrainHead + int64_t(kCls) * a.rows;
@@ -1093,15 +1095,15 @@ void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
     };
     auto mark = [&](int i) { if (a.drain_ev) (void)hipEventRecord(a.drain_ev[i], st); };
     mark(0);
-#define GSP_DRAIN_LDS(C, NT, CAP, PER_CU)                                                           \
+#define GSP_DRAIN_LDS(C, NT, CAP, PER_CU, W)                                                        \
     if (const unsigned g = grid(C, PER_CU))                                                           \
-        hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, NT, CAP, C>), dim3(g), dim3(NT), 0, st, a);   \
+        hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, NT, CAP, C, W>), dim3(g), dim3(NT), 0, st, a); \
     mark(C + 1);
     // class c: rows of at most CAP update tuples (pv_drain_class), PER_CU rows per CU by LDS
-    GSP_DRAIN_LDS(0, 192, 3072, 5)
-    GSP_DRAIN_LDS(1, 256, 4096, 4)
-    GSP_DRAIN_LDS(2, 512, 8192, 2)
-    GSP_DRAIN_LDS(3, 1024, kDrainLdsMax, 1)
+    GSP_DRAIN_LDS(0, 192, kDrainCap0, kDrainPerCU0, kDrainWaves0)
+    GSP_DRAIN_LDS(1, 256, 4096, 4, 4)
+    GSP_DRAIN_LDS(2, 512, 8192, 2, 4)
+    GSP_DRAIN_LDS(3, 1024, kDrainLdsMax, 1, 4)
 #undef GSP_DRAIN_LDS
     if (grid(kDrainHub, 1)) hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(grid(kDrainHub, 1)), dim3(kHT), 0, st, a);
     mark(kDrainHub + 1);

@@ -106,6 +106,9 @@ constexpr int kDrainHub = 4;
 constexpr int kDrainHead = 16;
 constexpr int kDrainStage = 64;
 constexpr int kDrainLdsMax = 16384;
+// class 0: tuples, rows per CU, waves per SIMD (round 6: 2,560 / 6 / 5 -- the k <= 8 rows alone,
+// 76 B of spills -- ran 5.05 ms of drain against 5.03)
+constexpr int kDrainCap0 = 3072, kDrainPerCU0 = 5, kDrainWaves0 = 4;
 // a hub row past its HBM buffers stops the job: err = tick | kDrainErrBit (kRowxErrBit: 1 << 24)
 constexpr int32_t kDrainErrBit = 1 << 25;
 __host__ __device__ inline int64_t pv_drain_need(int32_t k, int32_t view) {
@@ -116,7 +119,7 @@ __host__ __device__ inline int64_t pv_drain_need(int32_t k, int32_t view) {
 __host__ __device__ inline int32_t pv_drain_class(int32_t k, int32_t view, int32_t lds, int32_t wide) {
     const int64_t need = pv_drain_need(k, view);
     if (view < 8 || k > kDrainStage || need > lds) return kDrainHub;
-    if (wide < 1 && need <= 3072) return 0;
+    if (wide < 1 && need <= kDrainCap0) return 0;
     if (wide < 2 && need <= 4096) return 1;
     if (wide < 3 && need <= 8192) return 2;
     return need <= kDrainLdsMax ? 3 : kDrainHub;
