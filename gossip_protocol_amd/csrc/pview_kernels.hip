@@ -1161,9 +1161,41 @@ __global__ void __launch_bounds__(256) pview_receipt_kernel(PviewReceiptArgs a) 
 template <int kF>
 __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     const int32_t lr = int32_t(blockIdx.x) * 256 + int32_t(threadIdx.x);
+    const uint32_t t = uint32_t(a.tick);
+    // TFAIL: peers and the probe target are chosen among the members not suspected at t, by
+    // rank in id order (an 8-word bitmap of the gossipable slots).  The wave builds its 64 rows'
+    // bitmaps together, every lane still active: row j is read coalesced (lane l takes slots
+    // l, l + 64, ...) and four ballots give its bitmap to lane j -- one lane reading its own 2 KB
+    // row slot by slot made every load touch 64 rows' lines (3.7 ms per tick at config 5)
+    uint32_t gmask[kPvMaxView / 32];
+#pragma unroll
+    for (int w = 0; w < kPvMaxView / 32; ++w) gmask[w] = 0u;
+    if (a.tfail > 0) {
+        const uint32_t t5 = t & 31u, tf = uint32_t(a.tfail);
+        const int32_t lane = int32_t(threadIdx.x) & 63, lr0 = lr - lane;
+        for (int32_t j0 = 0; j0 < 64; j0 += 4) {                 // 4 rows' loads in flight
+            uint64_t e[4][kPvMaxView / 64];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < kPvMaxView / 64; ++c) {
+                    const int32_t lj = lr0 + j0 + u, i = c * 64 + lane;
+                    e[u][c] = lj < a.rows && i < a.view ? a.cur[int64_t(lj) * a.view + i] : kPvEmpty;
+                }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int c = 0; c < kPvMaxView / 64; ++c) {
+                    const uint64_t b = __ballot(e[u][c] != kPvEmpty && ((t5 - uint32_t(e[u][c])) & 31u) < tf);
+                    if (lane == j0 + u) {
+                        gmask[2 * c] = uint32_t(b);
+                        gmask[2 * c + 1] = uint32_t(b >> 32);
+                    }
+                }
+        }
+    }
     if (lr >= a.rows) return;
     const int32_t r = a.row0 + lr, F = a.fanout;
-    const uint32_t t = uint32_t(a.tick);
     unsigned long long *w3 = a.rowdig + int64_t(lr) * 16 + 3;
     const bool dead = a.tick > a.fail_tick[r] || (a.start_tick && a.tick < a.start_tick[r]) ||
                       (a.tick > 0 && *a.err);
@@ -1176,22 +1208,15 @@ __global__ void __launch_bounds__(256) pview_send_kernel(PviewTickArgs a) {
     }
     const int32_t len = a.len_cur[lr];
     const uint64_t *row = a.cur + int64_t(lr) * a.view;
-    // TFAIL: peers and the probe target are chosen among the members not suspected at t,
-    // by rank in id order (an 8-word bitmap of the gossipable slots)
-    uint32_t gmask[kPvMaxView / 32];
     int32_t cnt = len;
     if (a.tfail > 0) {
         cnt = 0;
-        const uint32_t t5 = t & 31u, tf = uint32_t(a.tfail);
 #pragma unroll
-        for (int w = 0; w < kPvMaxView / 32; ++w) {
-            uint32_t m = 0;
-            for (int b = 0; b < 32; ++b) {
-                const int32_t i = w * 32 + b;
-                if (i < len && ((t5 - uint32_t(row[i])) & 31u) < tf) m |= 1u << b;
-            }
-            gmask[w] = m;
-            cnt += __builtin_popcount(m);
+        for (int w = 0; w < kPvMaxView / 32; ++w) {              // slots past len are empty
+            const int32_t lo = w * 32;
+            const uint32_t keep = len >= lo + 32 ? ~0u : len <= lo ? 0u : (1u << (len - lo)) - 1u;
+            gmask[w] &= keep;
+            cnt += __builtin_popcount(gmask[w]);
         }
     }
     auto slot_of = [&](int32_t rk) -> int32_t {     // rank among the gossipable -> slot
