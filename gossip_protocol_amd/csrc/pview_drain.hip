@@ -432,6 +432,9 @@ __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, in
             surv += rm ? 0u : 1u;
             if (jn) hsum += pv_hash(uint32_t(Sj), x);
             if (rm) hsum += pv_hash(uint32_t(Sr), x);
+            // the eviction's first histogram (zeroed at the row's start): a long row's list
+            // nearly always holds more than V survivors
+            else atomicAdd(&sh.hist[d_prefix(v, t5) >> 8], 1u);
         }
         if (ev) {
             const bool ej = jn && (a.ev.kinds & GSP_EVENTS_JOIN), er = rm && (a.ev.kinds & GSP_EVENTS_REMOVE);
@@ -447,57 +450,51 @@ __device__ __forceinline__ void d_finish(const PviewTickArgs &a, Sh &sh, P S, in
     // survivor with a smaller prefix is kept
     uint32_t T16 = 0x10000u, need2 = 0;
     if (int32_t(C) > V) {
-        for (int pass = 0; pass < 2; ++pass) {
-            for (int32_t i = tid; i < 256; i += NT) sh.hist[i] = 0;
-            __syncthreads();
-            const uint32_t hi = pass ? T16 : 0u;
-            for (int32_t i = tid; i < L; i += NT) {
-                const uint32_t v = uint32_t(S[i]) & 0xFFFFu;
-                if (((t5 - v) & 31u) >= tr) continue;
-                const uint32_t p = d_prefix(v, t5);
-                if (pass == 0) atomicAdd(&sh.hist[p >> 8], 1u);
-                else if ((p >> 8) == hi) atomicAdd(&sh.hist[p & 255u], 1u);
-            }
-            __syncthreads();
-            d_select(sh, pass ? need2 : uint32_t(V));
-            if (pass == 0) { T16 = sh.sel[0]; need2 = sh.sel[1]; }
-            else { T16 = (T16 << 8) | sh.sel[0]; need2 = sh.sel[1]; }
-            __syncthreads();                                     // sel / hist reused
+        d_select(sh, uint32_t(V));                               // the high byte (built above)
+        T16 = sh.sel[0];
+        need2 = sh.sel[1];
+        __syncthreads();                                         // sel / hist reused
+        for (int32_t i = tid; i < 256; i += NT) sh.hist[i] = 0;
+        __syncthreads();
+        for (int32_t i = tid; i < L; i += NT) {                  // the low byte, that bin only
+            const uint32_t v = uint32_t(S[i]) & 0xFFFFu;
+            if (((t5 - v) & 31u) >= tr) continue;
+            const uint32_t p = d_prefix(v, t5);
+            if ((p >> 8) == T16) atomicAdd(&sh.hist[p & 255u], 1u);
         }
+        __syncthreads();
+        d_select(sh, need2);
+        T16 = (T16 << 8) | sh.sel[0];
+        need2 = sh.sel[1];
     }
     pm.mark(6);
     // the kept entries in id order: contiguous pieces per lane.  The T16 bin's members are
     // kept in (rotated) id order: member rank rho (id order) -> (rho - MB) mod c2, MB = the
     // members below the rotation point
     const int32_t F = (L + NT - 1) / NT, i0 = tid * F, i1 = i0 + F < L ? i0 + F : L;
-    uint32_t mc = 0, mb = 0;
-    if (T16 < 0x10000u)
-        for (int32_t i = i0; i < i1; ++i) {
-            const uint64_t e = S[i];
-            const uint32_t v = uint32_t(e) & 0xFFFFu;
-            if (((t5 - v) & 31u) < tr && d_prefix(v, t5) == T16) {
-                mc++;
-                mb += uint32_t(e >> 32) < mrot ? 1u : 0u;
-            }
+    uint32_t mc = 0, mb = 0, less = 0;                           // less: survivors below T16
+    for (int32_t i = i0; i < i1; ++i) {
+        const uint64_t e = S[i];
+        const uint32_t v = uint32_t(e) & 0xFFFFu;
+        if (((t5 - v) & 31u) >= tr) continue;
+        const uint32_t p = d_prefix(v, t5);
+        less += p < T16 ? 1u : 0u;
+        if (p == T16) {
+            mc++;
+            mb += uint32_t(e >> 32) < mrot ? 1u : 0u;
         }
+    }
     uint32_t c2 = 0, MB = 0;
     const uint32_t rho0 = d_scan<NT>(mc, &c2, sh.red[1]);
     MB = d_sum<NT>(mb, sh.red[0]);
-    uint32_t kept = 0;
-    {
-        uint32_t rho = rho0;
-        for (int32_t i = i0; i < i1; ++i) {
-            const uint32_t v = uint32_t(S[i]) & 0xFFFFu;
-            if (((t5 - v) & 31u) >= tr) continue;
-            const uint32_t p = d_prefix(v, t5);
-            if (p < T16) kept++;
-            else if (p == T16) {
-                const uint32_t rr = rho >= MB ? rho - MB : rho + c2 - MB;
-                kept += rr < need2 ? 1u : 0u;
-                rho++;
-            }
-        }
-    }
+    // the lane's members are ranks [rho0, rho0 + mc); rank rho is kept iff (rho - MB) mod c2 <
+    // need2, i.e. rho in [MB, min(c2, MB + need2)) or in [0, MB + need2 - c2)
+    auto overlap = [](uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) -> uint32_t {
+        const uint32_t lo = a0 > b0 ? a0 : b0, hi = a1 < b1 ? a1 : b1;
+        return hi > lo ? hi - lo : 0u;
+    };
+    const uint32_t kend = MB + need2 < c2 ? MB + need2 : c2, kwrap = MB + need2 > c2 ? MB + need2 - c2 : 0u;
+    const uint32_t kept = less + overlap(rho0, rho0 + mc, MB, kend) + overlap(rho0, rho0 + mc, 0u, kwrap);
     uint32_t W = 0;
     const uint32_t w0 = d_scan<NT>(kept, &W, sh.red[1]);
     uint64_t *out = a.cur + int64_t(lr) * V;
@@ -777,6 +774,7 @@ __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<k
     while ((1 << lgV) < V) ++lgV;
     const int32_t Vp = 1 << lgV;
     int64_t xo = 0;
+    for (int32_t i = tid; i < 256; i += kHT) sh.hist[i] = 0;     // d_finish's first histogram
     int32_t L = d_own<kHT>(a, sh, base, lr, r);
     pm.mark(1);
     uint32_t merged = 0;
@@ -1036,6 +1034,7 @@ __device__ __forceinline__ void d_row_lds(const PviewTickArgs &a, DrainShared<NT
     const uint32_t t5 = uint32_t(a.tick) & 31u, tr = uint32_t(a.tremove);
     DMark pm;
     pm.init(a.prof, it, k);
+    for (int32_t i = tid; i < 256; i += NT) sh.hist[i] = 0;     // d_finish's first histogram
     d_rank_stage<NT>(a, cur, reinterpret_cast<uint32_t *>(sh.buf), sh.stage);   // 1. ascending senders
     d_fetch_row(a, nxt);
     uint32_t pcol;
