@@ -85,6 +85,8 @@ struct gsp_pview {
     int32_t cus = 0;             // compute units (drain grid)
     int32_t *h_kcount = nullptr; // pinned [8]: the bucket sizes, the split kernels' grids
     hipEvent_t kcount_ev = nullptr;
+    hipStream_t drain_st = nullptr;     // drain all, split form: the drain classes' stream
+    hipEvent_t drain_fork = nullptr, drain_join = nullptr;   // (GSP_TEST_PV_DRAIN_STREAM=1 only)
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_TEST_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
@@ -165,6 +167,9 @@ struct gsp_pview {
         a.split = split;
         a.kcount_host = h_kcount;
         a.kcount_event = kcount_ev;
+        a.drain_st = drain_st;
+        a.drain_fork = drain_fork;
+        a.drain_join = drain_join;
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
@@ -478,6 +483,13 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
         GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
         if (p->inbox == 0) GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_dhead), gsp::kDrainHead * 4));
+        // opt-in (A/B, DESIGN.md 4b: the side stream ran 10.07 ms against 9.18 ms of tick kernels)
+        const char *ds = std::getenv("GSP_TEST_PV_DRAIN_STREAM");
+        if (p->inbox == 0 && ds && std::atoi(ds)) {
+            GSP_HIP(hipStreamCreateWithFlags(&s->drain_st, hipStreamNonBlocking));
+            GSP_HIP(hipEventCreateWithFlags(&s->drain_fork, hipEventDisableTiming));
+            GSP_HIP(hipEventCreateWithFlags(&s->drain_join, hipEventDisableTiming));
+        }
         s->nowait = s->rowmode;
         if (const char *nw = std::getenv("GSP_TEST_PV_NOWAIT")) s->nowait = std::atoi(nw) != 0;
         if (s->nowait && p->inbox == 0)
@@ -614,6 +626,9 @@ int gsp_pview_destroy(gsp_pview *s) {
     if (s->h_dhead) (void)hipHostFree(s->h_dhead);
     if (s->h_dring) (void)hipHostFree(s->h_dring);
     if (s->kcount_ev) (void)hipEventDestroy(s->kcount_ev);
+    if (s->drain_fork) (void)hipEventDestroy(s->drain_fork);
+    if (s->drain_join) (void)hipEventDestroy(s->drain_join);
+    if (s->drain_st) (void)hipStreamDestroy(s->drain_st);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return GSP_OK;

@@ -1425,6 +1425,16 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         GSP_PV_RANGE(E, 128, 4, 4, 7, true, g4)                                                         \
         GSP_PV_RANGE(E, 128, 0, 3, 8, false, g03)                                                       \
     } while (0)
+        // drain all: the long rows' classes may go first on their own stream (their rows and the
+        // split kernels' are disjoint); measured slower than one stream, opt-in
+        const bool side = a.drain && a.drain_st && a.drain_fork && a.drain_join;
+        if (side) {
+            if (hipEventRecord(a.drain_fork, st) != hipSuccess ||
+                hipStreamWaitEvent(a.drain_st, a.drain_fork, 0) != hipSuccess)
+                return hipGetLastError();
+            const hipError_t e = launch_pview_drain(b, a.drain_st);
+            if (e != hipSuccess) return e;
+        }
         switch (ext) {      // evict_order 1: the plain protocol's kernel, or the superset one
             case 0: GSP_PV_SPLIT_LAUNCH(0); break;
             case kExtEv: GSP_PV_SPLIT_LAUNCH(kExtEv); break;
@@ -1435,7 +1445,11 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         }
 #undef GSP_PV_SPLIT_LAUNCH
 #undef GSP_PV_RANGE
-        if (a.drain) {
+        if (side) {
+            if (hipEventRecord(a.drain_join, a.drain_st) != hipSuccess ||
+                hipStreamWaitEvent(st, a.drain_join, 0) != hipSuccess)
+                return hipGetLastError();
+        } else if (a.drain) {
             const hipError_t e = launch_pview_drain(b, st);
             if (e != hipSuccess) return e;
         }

@@ -90,6 +90,9 @@ struct PviewTickArgs {
                                  // exit at once), the drain classes on persistent grids
     int32_t *dhead_async;        // nowait + drain all: pinned [kDrainHead], long_list's head copied
                                  // without a wait (the engine reads it after its next sync), or null
+    hipStream_t drain_st;        // split form: the drain classes run on this stream beside the split
+    hipEvent_t drain_fork, drain_join;   // kernels (fork after the receipt, join before the send
+                                         // kernel), or null: on the tick's stream after them
     hipEvent_t *drain_ev;        // [kDrainClasses + 1]: recorded before the first drain class and
                                  // after each (the per-class kernel time), or null
 };
