@@ -1084,7 +1084,7 @@ __global__ void __launch_bounds__(NT, kWaves) pview_drain_lds_kernel(PviewTickAr
 }
 
 template <bool kEv>
-void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
+void launch_drain_classes(const PviewTickArgs &a, hipStream_t st, int parts) {
     const unsigned cus = unsigned(a.cus);
     // grid: the class's rows when the host knows them (zero: no launch), else persistent
     auto grid = [&](int c, unsigned per_cu) -> unsigned {
@@ -1093,7 +1093,8 @@ void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
         return unsigned(rows < int32_t(per_cu * cus) ? rows : int32_t(per_cu * cus));
     };
     auto mark = [&](int i) { if (a.drain_ev) (void)hipEventRecord(a.drain_ev[i], st); };
-    mark(0);
+    if (parts & 1) {
+        mark(0);
 #define GSP_DRAIN_LDS(C, NT, CAP, PER_CU, W)                                                        \
     if (const unsigned g = grid(C, PER_CU))                                                           \
         hipLaunchKernelGGL((pview_drain_lds_kernel<kEv, NT, CAP, C, W>), dim3(g), dim3(NT), 0, st, a); \
@@ -1104,19 +1105,24 @@ void launch_drain_classes(const PviewTickArgs &a, hipStream_t st) {
     GSP_DRAIN_LDS(2, 512, 8192, 2, 4)
     GSP_DRAIN_LDS(3, 1024, kDrainLdsMax, 1, 4)
 #undef GSP_DRAIN_LDS
-    if (grid(kDrainHub, 1)) hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(grid(kDrainHub, 1)), dim3(kHT), 0, st, a);
-    mark(kDrainHub + 1);
+    }
+    if (parts & 2) {
+        // on a stream of its own (parts == 2) the hub kernel's interval starts at its own event
+        if (parts == 2 && a.drain_ev) (void)hipEventRecord(a.drain_ev[kDrainClasses + 1], st);
+        if (grid(kDrainHub, 1)) hipLaunchKernelGGL((pview_drain_hbm_kernel<kEv>), dim3(grid(kDrainHub, 1)), dim3(kHT), 0, st, a);
+        mark(kDrainHub + 1);
+    }
 }
 
 }  // namespace
 
-hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st) {
+hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st, int parts) {
     if (!a.drain || a.rows == 0) return hipSuccess;
     if (!a.long_list || !a.scratch || a.cus < 1 || a.scratch_cap < 8192 || a.drain_lds < 1 ||
         a.drain_lds > kDrainLdsMax)
         return hipErrorInvalidValue;
-    if (a.ev.buf) launch_drain_classes<true>(a, st);
-    else launch_drain_classes<false>(a, st);
+    if (a.ev.buf) launch_drain_classes<true>(a, st, parts);
+    else launch_drain_classes<false>(a, st, parts);
     return hipGetLastError();
 }
 

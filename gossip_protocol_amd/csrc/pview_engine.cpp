@@ -86,7 +86,8 @@ struct gsp_pview {
     int32_t *h_kcount = nullptr; // pinned [8]: the bucket sizes, the split kernels' grids
     hipEvent_t kcount_ev = nullptr;
     hipStream_t drain_st = nullptr;     // drain all, split form: the drain classes' stream
-    hipEvent_t drain_fork = nullptr, drain_join = nullptr;   // (GSP_TEST_PV_DRAIN_STREAM=1 only)
+    hipEvent_t drain_fork = nullptr, drain_join = nullptr;   // (GSP_TEST_PV_DRAIN_STREAM=1 / 2 only)
+    int32_t drain_side = 0;      // 1 every drain class on drain_st, 2 the hub kernel only
     int32_t max_segment = gsp::kPvMaxSegment;
     bool sort_rows = true;       // run rows k-descending (GSP_TEST_PV_SORT=0 turns it off)
     bool drain = false;          // inbox 0: every message merged (pview_drain.hip)
@@ -100,7 +101,8 @@ struct gsp_pview {
     int32_t *h_dring = nullptr;  // nowait + drain all: pinned [max_ticks + 1][local shards][kDrainHead]
     std::vector<std::pair<int32_t, int32_t>> dring_pending;   // (tick, local shard) heads to add
     // drain all: per class, rows and messages run and kernel ms (gsp_pview_drain_stats)
-    using DrainEvents = std::array<hipEvent_t, gsp::kDrainClasses + 1>;
+    // class c runs from [c] to [c + 1]; the hub kernel on its own stream from [kDrainClasses + 1]
+    using DrainEvents = std::array<hipEvent_t, gsp::kDrainClasses + 2>;
     std::vector<DrainEvents> dpending;
     int64_t drain_rows[gsp::kDrainClasses] = {}, drain_msgs[gsp::kDrainClasses] = {};
     double drain_ms[gsp::kDrainClasses] = {};
@@ -170,6 +172,7 @@ struct gsp_pview {
         a.drain_st = drain_st;
         a.drain_fork = drain_fork;
         a.drain_join = drain_join;
+        a.drain_side = drain_side;
         a.rows_run = sh.rows_run.p ? sh.rows_run.p + t : nullptr;
         a.evict_rot = p.evict_order;
         a.ev = sh.ev.args();
@@ -438,7 +441,8 @@ int pview_collect(gsp_pview *s) {
         GSP_HIP(hipEventSynchronize(de[gsp::kDrainClasses]));
         for (int c = 0; c < gsp::kDrainClasses; ++c) {
             float ms = 0.f;
-            GSP_HIP(hipEventElapsedTime(&ms, de[size_t(c)], de[size_t(c) + 1]));
+            const size_t c0 = c == gsp::kDrainHub && s->drain_side == 2 ? size_t(gsp::kDrainClasses) + 1 : size_t(c);
+            GSP_HIP(hipEventElapsedTime(&ms, de[c0], de[size_t(c) + 1]));
             s->drain_ms[c] += ms;
         }
         for (hipEvent_t e : de) s->free_events.push_back(e);
@@ -483,9 +487,14 @@ int pview_build(const gsp_pview_params *p, int device, int32_t shards, int32_t r
         GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_kcount), 8 * 4));
         GSP_HIP(hipEventCreateWithFlags(&s->kcount_ev, hipEventDisableTiming));
         if (p->inbox == 0) GSP_HIP(hipHostMalloc(reinterpret_cast<void **>(&s->h_dhead), gsp::kDrainHead * 4));
-        // opt-in (A/B, DESIGN.md 4b: the side stream ran 10.07 ms against 9.18 ms of tick kernels)
+        // drain all: the hub kernel on a stream of its own beside the split kernels and the LDS
+        // classes (few hub rows, one per CU, would leave the rest of the GPU idle); tests / A/B:
+        // GSP_TEST_PV_DRAIN_STREAM=0 one stream, =1 every drain class on the side stream (slower,
+        // DESIGN.md 4b)
         const char *ds = std::getenv("GSP_TEST_PV_DRAIN_STREAM");
-        if (p->inbox == 0 && ds && std::atoi(ds)) {
+        const int dmode = ds ? std::atoi(ds) : 2;
+        if (p->inbox == 0 && dmode) {
+            s->drain_side = dmode == 1 ? 1 : 2;
             GSP_HIP(hipStreamCreateWithFlags(&s->drain_st, hipStreamNonBlocking));
             GSP_HIP(hipEventCreateWithFlags(&s->drain_fork, hipEventDisableTiming));
             GSP_HIP(hipEventCreateWithFlags(&s->drain_join, hipEventDisableTiming));

@@ -1425,14 +1425,15 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         GSP_PV_RANGE(E, 128, 4, 4, 7, true, g4)                                                         \
         GSP_PV_RANGE(E, 128, 0, 3, 8, false, g03)                                                       \
     } while (0)
-        // drain all: the long rows' classes may go first on their own stream (their rows and the
-        // split kernels' are disjoint); measured slower than one stream, opt-in
+        // drain all: the hub kernel goes first on a stream of its own (its rows and the others'
+        // are disjoint): a tick's few hub rows run one per CU and would leave the rest of the GPU
+        // idle behind them; every drain class there (drain_side 1) was slower
         const bool side = a.drain && a.drain_st && a.drain_fork && a.drain_join;
         if (side) {
             if (hipEventRecord(a.drain_fork, st) != hipSuccess ||
                 hipStreamWaitEvent(a.drain_st, a.drain_fork, 0) != hipSuccess)
                 return hipGetLastError();
-            const hipError_t e = launch_pview_drain(b, a.drain_st);
+            const hipError_t e = launch_pview_drain(b, a.drain_st, a.drain_side == 2 ? 2 : 3);
             if (e != hipSuccess) return e;
         }
         switch (ext) {      // evict_order 1: the plain protocol's kernel, or the superset one
@@ -1445,6 +1446,10 @@ hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st) {
         }
 #undef GSP_PV_SPLIT_LAUNCH
 #undef GSP_PV_RANGE
+        if (side && a.drain_side == 2) {                 // the LDS classes after the split kernels
+            const hipError_t e = launch_pview_drain(b, st, 1);
+            if (e != hipSuccess) return e;
+        }
         if (side) {
             if (hipEventRecord(a.drain_join, a.drain_st) != hipSuccess ||
                 hipStreamWaitEvent(st, a.drain_join, 0) != hipSuccess)

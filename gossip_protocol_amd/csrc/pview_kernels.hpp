@@ -93,8 +93,10 @@ struct PviewTickArgs {
     hipStream_t drain_st;        // split form: the drain classes run on this stream beside the split
     hipEvent_t drain_fork, drain_join;   // kernels (fork after the receipt, join before the send
                                          // kernel), or null: on the tick's stream after them
-    hipEvent_t *drain_ev;        // [kDrainClasses + 1]: recorded before the first drain class and
-                                 // after each (the per-class kernel time), or null
+    int32_t drain_side;          // with drain_st: 1 every drain class there, 2 the hub kernel only
+    hipEvent_t *drain_ev;        // [kDrainClasses + 2]: recorded before the first drain class and
+                                 // after each (the per-class kernel time; [kDrainClasses + 1]: the
+                                 // hub kernel's start on its own stream), or null
 };
 
 // Drain-all row classes (pview_drain.hip), by the row's update tuples: own view + k payloads
@@ -147,7 +149,8 @@ hipError_t launch_pview_receipt(const PviewReceiptArgs &a, hipStream_t st);
 // tick kernel, then the send kernel (peers, drops) and the digest reduction
 hipError_t launch_pview_tick(const PviewTickArgs &a, hipStream_t st);
 // drain-all rows (a.drain): launched by launch_pview_tick after the tick kernels
-hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st);
+// parts: 1 the LDS classes, 2 the hub kernel, 3 both
+hipError_t launch_pview_drain(const PviewTickArgs &a, hipStream_t st, int parts = 3);
 // receiver CSR of one shard from the send kernel's positions: csr_src[off[d] + pos] = sender
 hipError_t launch_pview_scatter(const int32_t *out_dst, const int32_t *out_pos, int64_t slots,
                                 int32_t fanout, const int32_t *off, int32_t *csr_src, hipStream_t st);
