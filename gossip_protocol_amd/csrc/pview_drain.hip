@@ -692,6 +692,54 @@ __device__ __forceinline__ void d_merge_ip(P X, int32_t N, int32_t Vp) {
     }
 }
 
+// Hub kernel, step 3 in HBM for runs of w >= E / 2: one merge level X -> Y per pass, every lane's
+// E outputs from windows of E tuples of each input loaded at once (a bitonic half-cleaner and a
+// register sort, as d_merge_ip) instead of one dependent load per output (d_merge_runs);
+// returns the offset of the sorted buffer.
+template <int E>
+__device__ __forceinline__ int64_t d_merge_runs_win(uint64_t *base, int64_t C, int64_t xo, int32_t N, int32_t w0) {
+    const int32_t tid = threadIdx.x;
+    for (int32_t w = w0; w < N; w <<= 1) {
+        const uint64_t *X = base + xo;
+        uint64_t *Y = base + (C - xo);
+        for (int32_t d0 = tid * E; d0 < N; d0 += kHT * E) {    // E divides 2w: one pair per lane
+            const int32_t p0 = d0 & ~(2 * w - 1);
+            const int32_t a1 = p0 + w < N ? p0 + w : N, b1 = p0 + 2 * w < N ? p0 + 2 * w : N;
+            const int32_t na = a1 - p0, nb = b1 - a1, d = d0 - p0;
+            const uint64_t *A = X + p0, *B = X + a1;
+            int32_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+            while (lo < hi) {                                    // merge path: A first on ties
+                const int32_t mid = (lo + hi) >> 1;
+                if (A[mid] <= B[d - 1 - mid]) lo = mid + 1; else hi = mid;
+            }
+            const int32_t i = lo, j = d - lo;
+            uint64_t o[E], bq[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                o[q] = i + q < na ? A[i + q] : kNone;
+                bq[q] = j + q < nb ? B[j + q] : kNone;
+            }
+#pragma unroll
+            for (int q = 0; q < E; ++q) {                        // the E smallest: bitonic
+                const uint64_t y = bq[E - 1 - q];
+                o[q] = o[q] < y ? o[q] : y;
+            }
+#pragma unroll
+            for (int h = E / 2; h > 0; h >>= 1)
+#pragma unroll
+                for (int q = 0; q < E; ++q)
+                    if ((q & h) == 0) d_cx(o[q], o[q + h]);
+            const int32_t n = b1 - d0 < E ? b1 - d0 : E;
+#pragma unroll
+            for (int q = 0; q < E; ++q)
+                if (q < n) Y[d0 + q] = o[q];
+        }
+        __syncthreads();
+        xo = C - xo;
+    }
+    return xo;
+}
+
 // Each id's run folded in place, over the tuples S[sb, sb + n) of a sorted sequence of N.
 // Pass 1: lane t loads its F tuples into registers (one batch of independent reads), folds the
 // runs that start among them in registers -- a run that continues past them is walked on in
@@ -808,7 +856,7 @@ __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<k
                 __syncthreads();
             }
         }
-        xo = d_merge_runs(base, C, xo, N, Vp >= 8 ? kHBlock : Vp);
+        xo = Vp >= 8 ? d_merge_runs_win<16>(base, C, xo, N, kHBlock) : d_merge_runs(base, C, xo, N, Vp);
         pm.mark(3);
         {                                                        // fold, blocks of 8 K tuples
             uint64_t *S2 = base + xo;
