@@ -11,6 +11,11 @@ cases (the sharded form of EmulNet::ENsend / ENrecv, /root/reference/EmulNet.cpp
                   ranks by grouped ncclSend / ncclRecv, counts by all-gather / broadcast,
                   node 0's row by ncclBroadcast (join schedule)
   pview_rows      partial view, row shards: the same exchange for sender views
+  pview_burst, rows_burst
+                  a join burst (step_rate 0.0005: most nodes start at one tick knowing only the
+                  introducer) -- the partial view drained (inbox 0) and the full view's rows: the
+                  sizes posted to RCCL from earlier ticks' counts must absorb the burst's growth
+                  (rowx_host.cpp's growth-aware margins)
   pview_capacity, rows_capacity
                   a test's segment bound (GSP_TEST_MAX_SEGMENT) that a receiver of one rank
                   passes first: every rank's sync() must raise GSP_ERR_CAPACITY at the same
@@ -61,11 +66,14 @@ def run(case):
     bad = []
     if case in ("pview_capacity", "rows_capacity"):
         return run_capacity(case, rank, world, dev, uid)
-    if case in ("columns_tiled", "rows"):
+    if case in ("columns_tiled", "rows", "rows_burst"):
         n = 8192
         kw = dict(fanout=3, drop_pct=10, fail_mode=RANDOM, fail_tick=4, fail_ppm=20000, seed=8,
                   tfail=5, swim=2)
         pol = dict(drop_window=(2, 9), step_rate=0.02, intro_list=4, fail_events=[(7, 3, 0)])
+        if case == "rows_burst":
+            kw = dict(fanout=3, drop_pct=10, fail_mode=RANDOM, fail_tick=6, fail_ppm=20000, seed=9)
+            pol = dict(step_rate=0.0005, intro_list=0)
         orc = ScaleOracle(n, policy=oracle_policy(**pol), **kw)
         eng = ScaleEngine(n, max_ticks=ticks, device=dev, rank=rank, world=world, nccl_id=uid,
                           tiles=2 if case == "columns_tiled" else 1,
@@ -84,10 +92,16 @@ def run(case):
         n = 20000
         kw = dict(view=64, fanout=3, inbox=5, drop_pct=10, fail_mode=2, fail_tick=5,
                   fail_ppm=50000, seed=13)
+        pol = None
+        if case == "pview_burst":
+            n = 6000
+            kw = dict(view=64, fanout=3, inbox=0, drop_pct=10, fail_mode=2, fail_tick=6,
+                      fail_ppm=20000, seed=43)
+            pol = dict(step_rate=0.0005, intro_list=0)
         from gossip_protocol_amd.pview import PviewEngine
-        orc = PviewOracle(n, **kw)
+        orc = PviewOracle(n, policy=oracle_policy(**pol) if pol else None, **kw)
         eng = PviewEngine(n, max_ticks=ticks, device=dev, rank=rank, world=world, nccl_id=uid,
-                          **kw)
+                          policy=make_policy(**pol) if pol else None, **kw)
         lo, hi = rank * n // world, (rank + 1) * n // world
         rows_mine = list(range(lo, hi, 37)) + [hi - 1]
     for t in range(1, ticks + 1):
@@ -96,7 +110,7 @@ def run(case):
         got = sum_digests(eng.digest(t))
         if got != want:
             bad.append(("digest", t, got, want))
-    if case in ("columns_tiled", "rows"):
+    if case in ("columns_tiled", "rows", "rows_burst"):
         try:
             _check_scale_rows(eng, orc, n, rows_mine, cols)
         except AssertionError as e:

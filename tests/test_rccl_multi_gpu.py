@@ -49,7 +49,7 @@ def _launch(case, world):
 
 
 @pytest.mark.parametrize("case", ["columns_tiled", "rows", "pview_rows", "pview_capacity",
-                                  "rows_capacity"])
+                                  "rows_capacity", "pview_burst", "rows_burst"])
 def test_two_ranks_match_the_oracle(case):
     if _gpus() < 2:
         pytest.skip("needs two GPUs (%d visible)" % _gpus())
@@ -60,6 +60,7 @@ def test_two_ranks_match_the_oracle(case):
 def test_rank_program_one_rank():
     """The same child program with one rank (the one-GPU boxes): every check but the xGMI
     bytes, so the multi-GPU test's own logic is exercised wherever a GPU exists."""
-    for case in ("columns_tiled", "rows", "pview_rows", "pview_capacity", "rows_capacity"):
+    for case in ("columns_tiled", "rows", "pview_rows", "pview_capacity", "rows_capacity",
+                 "pview_burst", "rows_burst"):
         for r in _launch(case, 1):
             assert r["bad"] == [], (case, r)
