@@ -159,29 +159,6 @@ __device__ void d_sort_segment(int32_t *src, int32_t *slot, int32_t k, int32_t P
     __syncthreads();
 }
 
-// The same for a short segment (k <= NT, the LDS classes): each lane ranks its key against all
-// k (distinct keys, broadcast LDS reads) and writes it at its rank -- two barriers instead of
-// the bitonic network's log^2 steps.
-template <int NT>
-__device__ void d_rank_segment(int32_t *src, int32_t *slot, int32_t k, int32_t row0, uint64_t *keys) {
-    const int32_t t = threadIdx.x;
-    uint64_t key = ~0ull;
-    if (t < k) {
-        const int32_t s = src[t];
-        const int32_t sl = slot ? slot[t] : s - row0;
-        key = (uint64_t(uint32_t(s + 1)) << 32) | uint64_t(uint32_t(sl));
-        keys[t] = key;
-    }
-    __syncthreads();
-    if (t < k) {
-        int32_t rank = 0;
-        for (int32_t j = 0; j < k; ++j) rank += keys[j] < key ? 1 : 0;
-        src[rank] = int32_t(uint32_t(key >> 32)) - 1;
-        if (slot) slot[rank] = int32_t(uint32_t(key));
-    }
-    __syncthreads();
-}
-
 // The staging word of sender i of a segment: s << 40 | kind bits | its row (local, or the
 // received row of a remote sender)
 __device__ __forceinline__ uint64_t d_stage_word(const PviewTickArgs &a, int32_t s, const int32_t *slot, int32_t i) {
