@@ -786,6 +786,77 @@ __device__ __forceinline__ int32_t d_fold_ip(Sh &sh, P S, int32_t N, uint32_t t5
     return d_fold_block<NT, F>(sh, S, 0, N, N, kNoId, 0, t5, tr);
 }
 
+// The hub kernel's fold of one block: the block's nb tuples of the sorted HBM sequence H[0, nrest)
+// staged in LDS (B) and folded there as d_fold_block does -- only a run that continues past the
+// block reads on in HBM -- and the results written compacted to Out[out0, ...) in HBM (behind
+// the block: out0 + results <= the block's start + nb).  Returns the results written.
+template <int NT, int F, class Sh>
+__device__ __forceinline__ int32_t d_fold_staged(Sh &sh, SkewBuf B, const uint64_t *H, int32_t nb, int32_t nrest,
+                                                 uint32_t prev0, uint64_t *Out, int32_t out0, uint32_t t5, uint32_t tr) {
+    for (int32_t i = int32_t(threadIdx.x); i < nb; i += NT) B[i] = H[i];
+    __syncthreads();
+    const int32_t i0 = int32_t(threadIdx.x) * F;
+    uint64_t tu[F];
+#pragma unroll
+    for (int q = 0; q < F; ++q) tu[q] = i0 + q < nb ? B[i0 + q] : kNone;
+    const uint32_t prev = threadIdx.x == 0 ? prev0 : i0 < nb ? uint32_t(B[i0 - 1] >> 32) : kNoId;
+    uint32_t cnt = 0;
+    uint32_t cur = 0, own = 0;                                   // the run being folded
+    int32_t at0 = -1;                                            // its first tuple (this lane's)
+#pragma unroll
+    for (int q = 0; q < F; ++q) {
+        const uint32_t x = uint32_t(tu[q] >> 32);
+        const uint32_t px = q == 0 ? prev : uint32_t(tu[q > 0 ? q - 1 : 0] >> 32);
+        if (x != px) {                                           // a run starts here
+            cur = 0;
+            own = 0;
+            at0 = x != kNoId ? q : -1;
+        }
+        if (at0 >= 0) d_apply(cur, own, uint32_t(tu[q]), t5, tr);
+        const bool last = q + 1 == F || i0 + q + 1 == nb;        // this lane's last tuple
+        const uint32_t nx = q + 1 < F ? uint32_t(tu[q + 1 < F ? q + 1 : q] >> 32) : kNoId;
+        if (at0 >= 0 && (last || nx != x)) {
+            if (last) {                                          // may continue past this lane: a hub's
+                // hot ids run for up to k tuples, read four at a time (past the block: in HBM)
+                for (int32_t j = i0 + q + 1; j < nrest; j += 4) {
+                    uint64_t u[4];
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        const int32_t jj = j + z;
+                        u[z] = jj < nrest ? (jj < nb ? B[jj] : H[jj]) : kNone;
+                    }
+                    bool stop = false;
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        stop = stop || uint32_t(u[z] >> 32) != x;
+                        if (!stop) d_apply(cur, own, uint32_t(u[z]), t5, tr);
+                    }
+                    if (stop) break;
+                }
+            }
+            B[i0 + at0] = d_tuple(x, 0u, cur ? own : 0u, cur);   // cur = 0: absent
+            cnt += cur ? 1u : 0u;
+            at0 = -1;
+        }
+    }
+    __syncthreads();                                             // every run folded
+    uint64_t res[F];
+#pragma unroll
+    for (int q = 0; q < F; ++q) {
+        const int32_t i = i0 + q;
+        const uint64_t t = i < nb ? B[i] : kNone;
+        const uint32_t lo = uint32_t(t);
+        res[q] = (t != kNone && (lo >> 17) == 0u && (lo & 0xFFFFu) != 0u) ? t : 0ull;
+    }
+    uint32_t tot = 0;
+    uint32_t at = uint32_t(out0) + d_scan<NT>(cnt, &tot, sh.red[0]);
+#pragma unroll
+    for (int q = 0; q < F; ++q)
+        if (res[q]) Out[int32_t(at++)] = res[q];
+    __syncthreads();                                             // B reused by the next block
+    return int32_t(tot);
+}
+
 // ---- hub kernel (class kDrainHub): two HBM tuple buffers per workgroup, messages in chunks --
 
 template <bool kEv>
@@ -835,15 +906,16 @@ __device__ __forceinline__ void d_body_hbm(const PviewTickArgs &a, DrainShared<k
         }
         xo = Vp >= 8 ? d_merge_runs_win<16>(base, C, xo, N, kHBlock) : d_merge_runs(base, C, xo, N, Vp);
         pm.mark(3);
-        {                                                        // fold, blocks of 8 K tuples
+        {                                                        // fold, LDS-staged blocks of 8 K tuples
             uint64_t *S2 = base + xo;
+            const SkewBuf B{sh.buf};
             int32_t out = 0;
             uint32_t carry = kNoId;
-            constexpr int kFB = kHT * 8;                         // 8 tuples per lane in HBM
+            constexpr int kFB = kHT * 8;                         // 8 tuples per lane (16: spills)
             for (int32_t b0 = 0; b0 < N; b0 += kFB) {
                 const int32_t nb = N - b0 < kFB ? N - b0 : kFB;
                 const uint32_t last_x = uint32_t(S2[b0 + nb - 1] >> 32);   // before any compaction
-                out += d_fold_block<kHT, 8>(sh, S2, b0, nb, N, carry, out, t5, tr);
+                out += d_fold_staged<kHT, 8>(sh, B, S2 + b0, nb, N - b0, carry, S2, out, t5, tr);
                 carry = last_x;
             }
             L = out;
