@@ -751,10 +751,17 @@ __device__ __forceinline__ int32_t d_fold_block(Sh &sh, P S, int32_t sb, int32_t
         const uint32_t nx = q + 1 < F ? uint32_t(tu[q + 1 < F ? q + 1 : q] >> 32) : kNoId;
         if (at0 >= 0 && (last || nx != x)) {
             if (last) {                                          // may continue past this lane
-                for (int32_t j = i0 + q + 1; j < N; ++j) {
-                    const uint64_t u = S[j];
-                    if (uint32_t(u >> 32) != x) break;
-                    d_apply(cur, own, uint32_t(u), t5, tr);
+                for (int32_t j = i0 + q + 1; j < N; j += 4) {    // read four at a time
+                    uint64_t u[4];
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) u[z] = j + z < N ? S[j + z] : kNone;
+                    bool stop = false;
+#pragma unroll
+                    for (int z = 0; z < 4; ++z) {
+                        stop = stop || uint32_t(u[z] >> 32) != x;
+                        if (!stop) d_apply(cur, own, uint32_t(u[z]), t5, tr);
+                    }
+                    if (stop) break;
                 }
             }
             S[i0 + at0] = d_tuple(x, 0u, cur ? own : 0u, cur);   // cur = 0: absent
